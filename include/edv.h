@@ -1,0 +1,96 @@
+/*
+ * edv.h -- C-ABI of the MI355X (gfx950) batch Ed25519 verifier (libedv.so).
+ *
+ * Drop-in boundary for Plenum's client-request authentication hot path.  In the
+ * reference every request signature ends in ONE call:
+ *
+ *   stp_core/crypto/nacl_wrappers.py:232-242  Verifier.verify(signature, msg)
+ *       -> VerifyKey.verify(signature + msg)           nacl_wrappers.py:86-108
+ *       -> libnacl.crypto_sign_open(sm, pk)            (libsodium 1.0.18)
+ *
+ * made once per signature from NaclAuthNr.authenticate_multi
+ * (plenum/server/client_authn.py:83-113) through DidVerifier.verify
+ * (plenum/common/verifier.py:54-55).  edv_verify_batch replaces a whole batch of
+ * those calls; the Python shim (indy-plenum_amd/nacl_wrappers.py, client_authn.py,
+ * req_authenticator.py) keeps the reference's per-request semantics above it.
+ *
+ * Verdict contract: accept[i] == 1 iff libsodium 1.0.18
+ * crypto_sign_ed25519_verify_detached(sig_i, msg_i, len_i, pk_i) == 0, bit for
+ * bit (strict S < L, small-order R/A blocklist, canonical A, cofactorless
+ * equation).  The reference's positional sig||msg split (crypto_sign_open on
+ * signature + msg) is applied by the caller before this layer (see
+ * INTEGRATION.md); every sig here is exactly 64 bytes.
+ *
+ * All entry points return 0 on success or a negative EDV_E_* code, never
+ * throw, and keep no pointer to caller memory after returning.
+ */
+#ifndef EDV_H
+#define EDV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EDV_OK 0
+#define EDV_E_ARG -1   /* bad argument (null pointer with n > 0, bad offsets) */
+#define EDV_E_NODEV -2 /* no usable gfx950 device in device_mask */
+#define EDV_E_HIP -3   /* HIP runtime error (text: edv_last_error) */
+#define EDV_E_OOM -4   /* device or pinned allocation failed */
+
+/*
+ * Verify n detached signatures held in HOST memory; synchronous.
+ *   sigs     n x 64 bytes (R || S), contiguous
+ *   pks      n x 32 bytes (A), contiguous
+ *   msgs     concatenated messages; message i = msgs[msg_off[i] .. msg_off[i+1])
+ *   msg_off  n + 1 non-decreasing byte offsets
+ *   accept   out: n bytes, 1 = accept, 0 = reject
+ *   device_mask  bit d selects HIP device d; 0 = all visible devices.  The batch is
+ *            split by request index into contiguous shards, one per device (no
+ *            inter-device traffic; each shard's accept bytes land in its slice).
+ * Replaces: a loop of nacl_wrappers.Verifier.verify (nacl_wrappers.py:232-242).
+ */
+int edv_verify_batch(const uint8_t *sigs, const uint8_t *pks, const uint8_t *msgs, const uint64_t *msg_off,
+                     uint64_t n, uint8_t *accept, uint32_t device_mask);
+
+/*
+ * Same verdicts for inputs already resident in device memory of `device`;
+ * asynchronous on `stream` (a hipStream_t, NULL = the library's own stream of
+ * that device, which is then synchronised before returning).  Offsets are
+ * absolute into d_msgs minus msg_base (so a shard may pass the global offset
+ * array slice unchanged).  d_msgs must be readable 16 bytes past the last
+ * message byte.
+ */
+int edv_verify_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
+                         const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept,
+                         int device, void *stream);
+
+/*
+ * Measurement helper for bench.py: launches the verify kernel `iters` times
+ * on device-resident inputs between two HIP events recorded on the kernel's
+ * own stream and returns the elapsed milliseconds of the whole region.
+ */
+int edv_time_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
+                       const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept, int device,
+                       int iters, float *ms_out);
+
+/* Number of visible gfx950 devices (0 if none). */
+int edv_device_count(void);
+
+/* Device memory helpers so a host without PyTorch can stage inputs. */
+int edv_dev_alloc(int device, uint64_t bytes, void **out);
+int edv_dev_free(int device, void *p);
+int edv_h2d(int device, void *dst, const void *src, uint64_t bytes);
+int edv_d2h(int device, void *dst, const void *src, uint64_t bytes);
+
+/* Library/version string, e.g. "edv 0.1.0 gfx950". */
+const char *edv_version(void);
+
+/* Text of the last error raised on the calling thread ("" if none). */
+const char *edv_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EDV_H */

@@ -1,0 +1,304 @@
+"""Client authenticators (plenum/server/client_authn.py:25-258) with a batch
+entry point that sends every signature of a client-inbox batch to the GPU in
+ONE edv call.
+
+Per-request semantics are the reference's, exactly:
+  NaclAuthNr.authenticate_multi   client_authn.py:83-113
+    - threshold defaults to len(signatures); fewer signatures -> InsufficientSignatures
+    - in dict order: b58decode(sig) (any error -> InvalidSignatureFormat),
+      serializeForSig, getVerkey (None -> CouldNotAuthenticate), verifier(...),
+      verify; stop once `threshold` correct signatures are collected, else
+      InsufficientCorrectSignatures(correct, threshold)
+  CoreAuthMixin.authenticate      client_authn.py:211-246
+authenticate_batch runs that loop in three phases: (1) host prep of every
+signature position, recording the exception a position would raise instead of
+raising it; (2) one GPU batch for all verify calls; (3) replay of the sequential
+loop per request over the precomputed verdicts, so exception precedence,
+early break and the returned identifier lists are unchanged.  Work done in
+phase 1 for positions the sequential loop would never reach is pure (base58,
+serialisation, state lookups) and its results are discarded.
+"""
+import json
+from abc import abstractmethod
+from hashlib import sha256
+from typing import Dict
+
+from . import base58
+from . import edv
+from .constants import (ACTION_TYPES, FEES, IDENTIFIER, QUERY_TYPES, ROLE, SIGNATURE, SIGNATURES, VERKEY,
+                        WRITE_TYPES)
+from .exceptions import (CouldNotAuthenticate, EmptyIdentifier, EmptySignature, InsufficientCorrectSignatures,
+                         InsufficientSignatures, InvalidSignatureFormat, MissingIdentifier, MissingSignature,
+                         UnknownIdentifier)
+from .signing_serializer import serialize_msg_for_signing
+from .verifier import DidVerifier, Verifier
+
+
+class ClientAuthNr:
+    """Interface for client authenticators (client_authn.py:25-78)."""
+
+    @abstractmethod
+    def authenticate(self, msg: Dict, identifier: str = None, signature: str = None) -> str:
+        """Authenticate msg; return the identifier or raise a SigningException."""
+
+    @abstractmethod
+    def authenticate_multi(self, msg: Dict, signatures: Dict[str, str], threshold: int = None):
+        """Return the identifiers whose signatures verified; raise if threshold is not met."""
+
+    @abstractmethod
+    def addIdr(self, identifier, verkey, role=None):
+        """Register an identifier and its verification key."""
+
+    @abstractmethod
+    def getVerkey(self, identifier):
+        """The verification key for an identifier."""
+
+
+class _Raise:
+    """A recorded exception: raised at replay time only if the sequential loop reaches it."""
+
+    __slots__ = ("exc", "cause")
+
+    def __init__(self, exc, cause=None):
+        self.exc = exc
+        self.cause = cause
+
+    def fire(self):
+        if self.cause is not None:
+            raise self.exc from self.cause
+        raise self.exc
+
+
+class _Plan:
+    """Phase-1 result for one authenticate_multi call."""
+
+    __slots__ = ("threshold", "steps", "early")
+
+    def __init__(self, threshold, steps, early=None):
+        self.threshold = threshold
+        self.steps = steps      # list of (_Raise) or (idr, vr, sig_bytes, ser, job_index)
+        self.early = early      # _Raise raised before the loop (InsufficientSignatures)
+
+
+class NaclAuthNr(ClientAuthNr):
+
+    def authenticate_multi(self, msg: Dict, signatures: Dict[str, str], threshold: int = None,
+                           verifier: Verifier = DidVerifier):
+        return self.authenticate_multi_batch([(msg, signatures, threshold, verifier)], raise_single=True)[0]
+
+    # ---------------------------------------------------------------- batch
+    def _plan_multi(self, msg, signatures, threshold, verifier, jobs):
+        num_sigs = len(signatures)
+        if threshold is not None:
+            if num_sigs < threshold:
+                return _Plan(threshold, [], _Raise(InsufficientSignatures(num_sigs, threshold)))
+        else:
+            threshold = num_sigs
+        steps = []
+        for idr, sig in signatures.items():
+            try:
+                sig = base58.b58decode(sig)
+            except Exception as ex:
+                steps.append(_Raise(InvalidSignatureFormat(), ex))
+                continue
+            try:
+                ser = self.serializeForSig(msg, identifier=idr)
+                verkey = self.getVerkey(idr)
+                if verkey is None:
+                    raise CouldNotAuthenticate('Can not find verkey for {}'.format(idr))
+                vr = verifier(verkey, identifier=idr)
+            except Exception as ex:  # raised by the reference at this position
+                steps.append(_Raise(ex))
+                continue
+            key = vr.batch_key() if hasattr(vr, "batch_key") else None
+            if hasattr(vr, "batch_key"):
+                if key is None:
+                    steps.append((idr, vr, sig, ser, -1))        # no key: verify() is False
+                else:
+                    steps.append((idr, vr, sig, ser, len(jobs)))
+                    jobs.append((sig, ser, key))
+            else:
+                steps.append((idr, vr, sig, ser, None))          # foreign verifier: call it
+        return _Plan(threshold, steps)
+
+    @staticmethod
+    def _replay(plan, verdicts):
+        if plan.early is not None:
+            plan.early.fire()
+        correct_sigs_from = []
+        for st in plan.steps:
+            if isinstance(st, _Raise):
+                st.fire()
+            idr, vr, sig, ser, j = st
+            if j is None:
+                ok = vr.verify(sig, ser)
+            elif j < 0:
+                ok = False
+            else:
+                ok = verdicts[j]
+            if ok:
+                correct_sigs_from.append(idr)
+                if len(correct_sigs_from) == plan.threshold:
+                    break
+        else:
+            raise InsufficientCorrectSignatures(len(correct_sigs_from), plan.threshold)
+        return correct_sigs_from
+
+    def authenticate_multi_batch(self, calls, raise_single=False):
+        """calls: list of (msg, signatures, threshold, verifier).  Returns one
+        entry per call: the identifier list, or the exception instance the
+        reference's authenticate_multi would have raised (re-raised directly
+        when raise_single is set and there is one call)."""
+        jobs = []
+        plans = []
+        for msg, signatures, threshold, verifier in calls:
+            plans.append(self._plan_multi(msg, signatures, threshold, verifier or DidVerifier, jobs))
+        verdicts = edv.open_batch(jobs) if jobs else []
+        out = []
+        for plan in plans:
+            if raise_single:
+                out.append(self._replay(plan, verdicts))
+                continue
+            try:
+                out.append(self._replay(plan, verdicts))
+            except Exception as ex:
+                out.append(ex)
+        return out
+
+    @abstractmethod
+    def addIdr(self, identifier, verkey, role=None):
+        pass
+
+    @abstractmethod
+    def getVerkey(self, identifier):
+        pass
+
+    def serializeForSig(self, msg, identifier=None, topLevelKeysToIgnore=None):
+        return serialize_msg_for_signing(msg, topLevelKeysToIgnore=topLevelKeysToIgnore)
+
+
+def nym_to_state_key(nym: str) -> bytes:
+    """DomainRequestHandler.nym_to_state_key (plenum/server/domain_req_handler.py:166-167)."""
+    return sha256(nym.encode()).digest()
+
+
+def get_nym_details(state, nym, isCommitted: bool = True):
+    """DomainRequestHandler.getNymDetails (domain_req_handler.py:158-163): JSON
+    value under sha256(nym) in the state, {} if absent."""
+    data = state.get(nym_to_state_key(nym), isCommitted) if state is not None else None
+    if not data:
+        return {}
+    return json.loads(data.decode() if isinstance(data, (bytes, bytearray)) else data)
+
+
+class SimpleAuthNr(NaclAuthNr):
+    """In-memory identifiers, then the (uncommitted) state (client_authn.py:128-168)."""
+
+    def __init__(self, state=None):
+        self.clients = {}  # type: Dict[str, Dict]
+        self.state = state
+
+    def addIdr(self, identifier, verkey, role=None):
+        self.clients[identifier] = {VERKEY: verkey, ROLE: role}
+
+    def getVerkey(self, identifier):
+        nym = self.clients.get(identifier)
+        if not nym:
+            nym = get_nym_details(self.state, identifier, isCommitted=False)
+            if not nym:
+                raise UnknownIdentifier(identifier)
+        return nym.get(VERKEY)
+
+    def authenticate(self, msg: Dict, identifier: str = None, signature: str = None):
+        signatures = {identifier: signature}
+        return self.authenticate_multi(msg, signatures=signatures)
+
+
+class CoreAuthMixin:
+    excluded_from_signing = {SIGNATURE, SIGNATURES, FEES}
+    write_types = WRITE_TYPES
+    query_types = QUERY_TYPES
+    action_types = ACTION_TYPES
+
+    def is_query(self, typ):
+        return typ in self.query_types
+
+    def is_write(self, typ):
+        return typ in self.write_types
+
+    @classmethod
+    def is_action(cls, typ):
+        return typ in cls.action_types
+
+    @staticmethod
+    def _extract_signature(msg):
+        if SIGNATURE not in msg:
+            raise MissingSignature
+        if not msg[SIGNATURE]:
+            raise EmptySignature
+        return msg[SIGNATURE]
+
+    @staticmethod
+    def _extract_identifier(msg):
+        if IDENTIFIER not in msg:
+            raise MissingIdentifier
+        if not msg[IDENTIFIER]:
+            raise EmptyIdentifier
+        return msg[IDENTIFIER]
+
+    def _prepare(self, req_data, identifier=None, signature=None):
+        """The pre-loop part of authenticate (client_authn.py:222-244):
+        -> (to_serialize, signatures) or raises."""
+        to_serialize = {k: v for k, v in req_data.items() if k not in self.excluded_from_signing}
+        if req_data.get(SIGNATURE) is None and req_data.get(SIGNATURES) is None and signature is None:
+            raise MissingSignature
+        if req_data.get(IDENTIFIER) and (req_data.get(SIGNATURE) or signature):
+            try:
+                identifier = identifier or self._extract_identifier(req_data)
+                signature = signature or self._extract_signature(req_data)
+                signatures = {identifier: signature}
+            except Exception as ex:
+                if ex in (MissingSignature, EmptySignature, MissingIdentifier, EmptyIdentifier):
+                    ex = ex(req_data.get(IDENTIFIER), req_data.get(SIGNATURE))
+                raise ex
+        else:
+            signatures = req_data[SIGNATURES]
+        return to_serialize, signatures
+
+    def authenticate(self, req_data, identifier: str = None, signature: str = None,
+                     verifier: Verifier = DidVerifier):
+        to_serialize, signatures = self._prepare(req_data, identifier, signature)
+        return self.authenticate_multi(to_serialize, signatures=signatures, verifier=verifier)
+
+    def authenticate_batch(self, reqs, verifier: Verifier = DidVerifier):
+        """Batch form of authenticate over a list of request dicts: one GPU
+        call for all of them.  Returns, per request, the identifier list or
+        the exception instance authenticate() would raise."""
+        out = [None] * len(reqs)
+        calls, where = [], []
+        for k, req in enumerate(reqs):
+            try:
+                to_serialize, signatures = self._prepare(req)
+            except Exception as ex:
+                out[k] = ex
+                continue
+            calls.append((to_serialize, signatures, None, verifier))
+            where.append(k)
+        for k, res in zip(where, self.authenticate_multi_batch(calls)):
+            out[k] = res
+        return out
+
+    def serializeForSig(self, msg, identifier=None, topLevelKeysToIgnore=None):
+        if not msg.get(IDENTIFIER):
+            msg = {**msg, IDENTIFIER: identifier}
+        return serialize_msg_for_signing(msg, topLevelKeysToIgnore=topLevelKeysToIgnore)
+
+
+class CoreAuthNr(CoreAuthMixin, SimpleAuthNr):
+    def __init__(self, state=None):
+        SimpleAuthNr.__init__(self, state)
+        CoreAuthMixin.__init__(self)
+
+
+# The name the integration docs use for the batch-capable core authenticator.
+GpuAuthNr = CoreAuthNr

@@ -1,0 +1,92 @@
+// edv_hostcheck.cpp -- TEST HARNESS ONLY.  Builds the kernel's own math and
+// per-signature algorithm (edv_math.h, edv_verify_core.h) as plain C++ so the
+// CPU test suite can check them against the oracle and Python big integers
+// without a GPU.  Nothing in the product path (libedv.so, the Python shim)
+// loads this library; it is not a fallback.
+#include <stdint.h>
+#include <string.h>
+#include <vector>
+#include "edv_verify_core.h"
+
+using namespace edv;
+
+namespace {
+struct HostATab {
+  ge_cached t[kAEntries];
+  void store(int e, const ge_cached& c) { t[e] = c; }
+  ge_cached load(int e) const { return t[e]; }
+};
+struct HostBTab {
+  std::vector<int32_t> w;
+  HostBTab() : w(kBEntries * kBStride) {
+    for (int j = 0; j < kBEntries; j++) btab_entry(w.data() + j * kBStride, j);
+  }
+  ge_precomp entry(int j) const { return precomp_from_words(w.data() + j * kBStride); }
+};
+const HostBTab& btab() {
+  static HostBTab b;
+  return b;
+}
+void load_words(uint32_t* w, const uint8_t* b, int n) {
+  for (int i = 0; i < n; i++) w[i] = uint32_t(b[4 * i]) | uint32_t(b[4 * i + 1]) << 8 | uint32_t(b[4 * i + 2]) << 16 | uint32_t(b[4 * i + 3]) << 24;
+}
+void store_words(uint8_t* b, const uint32_t* w, int n) {
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < 4; j++) b[4 * i + j] = uint8_t(w[i] >> (8 * j));
+}
+fe to_fe(const int32_t* l) { fe f; for (int i = 0; i < 10; i++) f.v[i] = l[i]; return f; }
+void from_fe(int32_t* l, const fe& f) { for (int i = 0; i < 10; i++) l[i] = f.v[i]; }
+}  // namespace
+
+extern "C" {
+void hc_fe_mul(const int32_t* f, const int32_t* g, int32_t* h) { from_fe(h, fe_mul(to_fe(f), to_fe(g))); }
+void hc_fe_sq(const int32_t* f, int32_t* h) { from_fe(h, fe_sq(to_fe(f))); }
+void hc_fe_sq2(const int32_t* f, int32_t* h) { from_fe(h, fe_sq2(to_fe(f))); }
+void hc_fe_carry32(const int32_t* f, int32_t* h) { from_fe(h, fe_carry32(to_fe(f))); }
+void hc_fe_invert(const int32_t* f, int32_t* h) { from_fe(h, fe_invert(to_fe(f))); }
+void hc_fe_pow22523(const int32_t* f, int32_t* h) { from_fe(h, fe_pow22523(to_fe(f))); }
+void hc_fe_tobytes(const int32_t* f, uint8_t* out) { uint32_t w[8]; fe_tobytes(w, to_fe(f)); store_words(out, w, 8); }
+void hc_fe_frombytes(const uint8_t* in, int32_t* h) { uint32_t w[8]; load_words(w, in, 8); from_fe(h, fe_frombytes(w)); }
+void hc_sc_reduce(const uint8_t* in64, uint8_t* out32) {
+  uint32_t w[16], o[8];
+  load_words(w, in64, 16);
+  sc_reduce(o, w);
+  store_words(out32, o, 8);
+}
+void hc_hram(const uint8_t* R, const uint8_t* A, const uint8_t* m, uint64_t mlen, uint8_t* out64) {
+  uint32_t r[8], a[8], o[16];
+  load_words(r, R, 8);
+  load_words(a, A, 8);
+  // msg_word reads whole aligned words up to 12 bytes past the end: pad a copy
+  std::vector<uint8_t> buf(mlen + 32, 0);
+  if (mlen) memcpy(buf.data() + 16, m, mlen);
+  hram(o, r, a, buf.data() + 16, mlen);
+  store_words(out64, o, 16);
+}
+int hc_decompress_negate(const uint8_t* in, uint8_t* out) {
+  uint32_t w[8], o[8];
+  load_words(w, in, 8);
+  ge_p3 p;
+  const bool ok = ge_frombytes_negate(p, w);
+  ge_p2_tobytes(o, ge_p3_to_p2(p));
+  store_words(out, o, 8);
+  return ok ? 0 : -1;
+}
+void hc_btab(int32_t* out) { memcpy(out, btab().w.data(), sizeof(int32_t) * kBEntries * kBStride); }
+int hc_verify_batch(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off, uint64_t n,
+                    uint8_t* accept) {
+  const HostBTab& bt = btab();
+  for (uint64_t i = 0; i < n; i++) {
+    uint32_t R[8], S[8], A[8];
+    load_words(R, sigs + 64 * i, 8);
+    load_words(S, sigs + 64 * i + 32, 8);
+    load_words(A, pks + 32 * i, 8);
+    const uint64_t mlen = off[i + 1] - off[i];
+    std::vector<uint8_t> buf(mlen + 32, 0);
+    if (mlen) memcpy(buf.data() + 16, msgs + off[i], mlen);
+    HostATab at;
+    accept[i] = verify_one(R, S, A, buf.data() + 16, mlen, at, bt) ? 1 : 0;
+  }
+  return 0;
+}
+}

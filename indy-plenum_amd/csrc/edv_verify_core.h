@@ -1,0 +1,220 @@
+// edv_verify_core.h -- the per-signature verification algorithm (one lane),
+// __host__ __device__ so the exact kernel logic is unit-tested on the CPU
+// (libedv_hostcheck.so, tests only) before it runs on gfx950.
+//
+// Follows libsodium 1.0.18 crypto_sign_ed25519_verify_detached, the function
+// behind the reference's only verify call site
+// (stp_core/crypto/nacl_wrappers.py:86-108 -> libnacl.crypto_sign_open);
+// SURVEY.md section 8a rows V2-V9.
+#pragma once
+#include "edv_math.h"
+
+namespace edv {
+
+constexpr int kAEntries = 8;   // per-lane table 1..8 x (-A), cached form
+constexpr int kBEntries = 129; // shared table 0..128 x B, affine precomp form
+constexpr int kBStride = 32;   // words per B entry (30 used; 128-byte aligned)
+
+// ------------------------------------------------------------- message words
+EDV_HD uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return uint32_t(((uint64_t(hi) << 32) | lo) >> (8 * sh));
+}
+// Big-endian SHA word of message bytes [q, q+8) with the SHA-512 pad byte 0x80
+// at mlen and zeros after it.  Reads whole aligned 32-bit words: the buffer must
+// be readable up to 12 bytes past the message end.
+EDV_HD uint64_t msg_word(const uint8_t* m, uint64_t mlen, uint64_t q) {
+  const int64_t rem = int64_t(mlen) - int64_t(q);
+  const int nvalid = rem <= 0 ? 0 : (rem >= 8 ? 8 : int(rem));
+  uint32_t lo = 0, hi = 0;
+  if (nvalid > 0) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(m + q);
+    const uint32_t sh = uint32_t(a & 3);
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(a - sh);
+    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
+    lo = alignbyte(d1, d0, sh);
+    hi = alignbyte(d2, d1, sh);
+  }
+  uint64_t v = (uint64_t(hi) << 32) | lo;  // little-endian byte order
+  if (nvalid < 8) {
+    v &= (uint64_t(1) << (8 * nvalid)) - 1;
+    if (rem >= 0) v |= uint64_t(0x80) << (8 * nvalid);
+  }
+  return be64_from_le_words(uint32_t(v), uint32_t(v >> 32));
+}
+
+// SHA-512(R || A || M) -> 16 little-endian words of the 64-byte digest (V6)
+EDV_HD void hram(uint32_t out[16], const uint32_t R[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen) {
+  uint64_t H[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                   0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  const uint64_t total = 64 + mlen;
+  const uint64_t nb = (total + 17 + 127) / 128;
+  uint64_t W[16];
+#pragma unroll
+  for (int t = 0; t < 4; t++) W[t] = be64_from_le_words(R[2 * t], R[2 * t + 1]);
+#pragma unroll
+  for (int t = 0; t < 4; t++) W[4 + t] = be64_from_le_words(A[2 * t], A[2 * t + 1]);
+#pragma unroll
+  for (int t = 8; t < 16; t++) W[t] = msg_word(m, mlen, uint64_t(8 * (t - 8)));
+  if (nb == 1) { W[14] = total >> 61; W[15] = total << 3; }
+  sha512_compress(H, W);
+#pragma unroll 1
+  for (uint64_t b = 1; b < nb; b++) {
+    const uint64_t q0 = 128 * b - 64;
+#pragma unroll
+    for (int t = 0; t < 16; t++) W[t] = msg_word(m, mlen, q0 + 8 * t);
+    if (b == nb - 1) { W[14] = total >> 61; W[15] = total << 3; }
+    sha512_compress(H, W);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    out[2 * i] = bswap32(uint32_t(H[i] >> 32));
+    out[2 * i + 1] = bswap32(uint32_t(H[i]));
+  }
+}
+
+// ------------------------------------------------------------ scalar recoding
+// h < L: 64 signed radix-16 digits in [-8, 7], packed 4-bit two's complement,
+// digit k at bits 4*(k%8) of word k/8.
+EDV_HD void recode4(uint32_t out[8], const uint32_t h[8]) {
+  int carry = 0;
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      int e = int((h[w] >> (4 * k)) & 15) + carry;
+      carry = (w == 7 && k == 7) ? 0 : ((e + 8) >> 4);
+      e -= carry * 16;
+      packed |= uint32_t(e & 15) << (4 * k);
+    }
+    out[w] = packed;
+  }
+}
+// S: 32 signed radix-256 digits in [-128, 127] (S < 2^253 keeps the top digit
+// <= 32; larger S is rejected by V2 and only has to stay in table bounds).
+EDV_HD void recode8(uint32_t out[8], const uint32_t s[8]) {
+  int carry = 0;
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int e = int((s[w] >> (8 * k)) & 255) + carry;
+      carry = (w == 7 && k == 3) ? 0 : ((e + 128) >> 8);
+      e -= carry * 256;
+      packed |= uint32_t(e & 255) << (8 * k);
+    }
+    out[w] = packed;
+  }
+}
+// shift a 256-bit little-endian word vector left by N bits (0 < N < 32)
+template <int N>
+EDV_HD void shl256(uint32_t v[8]) {
+#pragma unroll
+  for (int i = 7; i > 0; i--) v[i] = (v[i] << N) | (v[i - 1] >> (32 - N));
+  v[0] <<= N;
+}
+
+EDV_HD ge_precomp precomp_from_words(const int32_t* w) {
+  ge_precomp q;
+#pragma unroll
+  for (int l = 0; l < 10; l++) { q.ypx.v[l] = w[l]; q.ymx.v[l] = w[10 + l]; q.xy2d.v[l] = w[20 + l]; }
+  return q;
+}
+
+// j * B for j in [0, 128], affine precomp form, written as kBStride words.
+EDV_HD void btab_entry(int32_t* o, int j) {
+  const uint32_t Bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                          0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+  ge_p3 nB;
+  ge_frombytes_negate(nB, Bw);
+  const ge_p3 B{fe_neg(nB.X), nB.Y, nB.Z, fe_neg(nB.T)};
+  const ge_cached Bc = ge_p3_to_cached(B);
+  ge_p3 acc = ge_p3_identity();
+  for (int bit = 7; bit >= 0; bit--) {
+    acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
+    if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add(acc, Bc));
+  }
+  const fe zi = fe_invert(acc.Z);
+  const fe x = fe_mul(acc.X, zi), y = fe_mul(acc.Y, zi);
+  const fe ypx = fe_carry32(fe_add(y, x)), ymx = fe_carry32(fe_sub(y, x));
+  const fe xy2d = fe_mul(fe_mul(x, y), fe_d2());
+  for (int l = 0; l < 10; l++) { o[l] = ypx.v[l]; o[10 + l] = ymx.v[l]; o[20 + l] = xy2d.v[l]; }
+  o[30] = 0;
+  o[31] = 0;
+}
+
+// The whole verdict for one signature.  ATab provides store(e, cached) /
+// load(e) for this lane's 1..8 x (-A) table; BTab provides entry(j) -> precomp.
+// Returns true iff libsodium's verify_detached would return 0.
+template <class ATab, class BTab>
+EDV_HD bool verify_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen,
+                       ATab& at, const BTab& bt) {
+  // V2-V4: strictness on bytes
+  bool ok = !((S[7] & 0xF0000000u) && !sc_is_canonical(S));
+  ok = ok && !has_small_order(R);
+  ok = ok && ge_is_canonical(A) && !has_small_order(A);
+  if (!ok) return false;
+  // V5
+  ge_p3 nA;
+  if (!ge_frombytes_negate(nA, A)) return false;
+  // V6, V7
+  uint32_t dig[16], h[8];
+  hram(dig, R, A, m, mlen);
+  sc_reduce(h, dig);
+  uint32_t hd[8], sd[8];
+  recode4(hd, h);
+  recode8(sd, S);
+  // table 1..8 x (-A)
+  {
+    const ge_cached c1 = ge_p3_to_cached(nA);
+    at.store(0, c1);
+    ge_p3 cur = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(nA)));
+    at.store(1, ge_p3_to_cached(cur));
+#pragma unroll 1
+    for (int e = 2; e < kAEntries; e++) {
+      cur = ge_p1p1_to_p3(ge_add(cur, c1));
+      at.store(e, ge_p3_to_cached(cur));
+    }
+  }
+  // V8: joint fixed-window double-scalar multiplication, top digit first.  Every
+  // lane adds at the same positions, so a wave never diverges here.
+  ge_p2 acc = ge_p2_identity();
+#pragma unroll 1
+  for (int w = 63; w >= 0; --w) {
+    ge_p3 p3;
+    if (w == 63) {
+      p3 = ge_p3_identity();
+    } else {
+      acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
+      acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
+      acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
+      p3 = ge_p1p1_to_p3(ge_p2_dbl(acc));
+    }
+    const int dA = int32_t(hd[7]) >> 28;
+    shl256<4>(hd);
+    const int ua = dA < 0 ? -dA : dA;
+    ge_cached c = at.load(ua == 0 ? 0 : ua - 1);
+    if (ua == 0) c = ge_cached_identity();
+    c = ge_cached_cneg(c, dA < 0);
+    ge_p1p1 t = ge_add(p3, c);
+    if ((w & 1) == 0) {
+      p3 = ge_p1p1_to_p3(t);
+      const int dB = int32_t(sd[7]) >> 24;
+      shl256<8>(sd);
+      const int ub = dB < 0 ? -dB : dB;
+      const ge_precomp q = ge_precomp_cneg(bt.entry(ub), dB < 0);
+      t = ge_madd(p3, q);
+    }
+    acc = ge_p1p1_to_p2(t);
+  }
+  // V9
+  uint32_t enc[8];
+  ge_p2_tobytes(enc, acc);
+  bool match = true;
+#pragma unroll
+  for (int k = 0; k < 8; k++) match = match && (enc[k] == R[k]);
+  return match;
+}
+
+}  // namespace edv

@@ -1,0 +1,206 @@
+"""ctypes binding of the gfx950 batch verifier C-ABI (include/edv.h, libedv.so).
+
+This is the thin shim between Plenum's authenticator layer (client_authn.py,
+req_authenticator.py, verifier.py, nacl_wrappers.py in this package) and the
+HIP kernels.  There is no CPU fallback here: if libedv.so is missing or no
+gfx950 device is visible, every call raises EdvUnavailable, loudly.
+
+Reference behaviour reproduced at this layer:
+  stp_core/crypto/nacl_wrappers.py:232-242  Verifier.verify(signature, msg)
+      -> crypto_sign_open(signature + msg, pk): the first 64 bytes of the
+         CONCATENATION are the signature and the rest is the message, so a
+         non-64-byte "signature" re-splits positionally (open_batch below);
+         fewer than 64 bytes in total rejects (libsodium: smlen < 64).
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("EDV_LIB", os.path.join(_HERE, "libedv.so"))
+
+EDV_OK = 0
+EDV_E_ARG = -1
+EDV_E_NODEV = -2
+EDV_E_HIP = -3
+EDV_E_OOM = -4
+
+
+class EdvUnavailable(RuntimeError):
+    """libedv.so cannot be loaded or no gfx950 device is visible."""
+
+
+class EdvError(RuntimeError):
+    """The C-ABI returned an error code."""
+
+    def __init__(self, code, what):
+        super().__init__("edv error {}: {}".format(code, what))
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib():
+    """The loaded libedv.so (raises EdvUnavailable if it is not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise EdvUnavailable("libedv.so not built at {} (run __graft_entry__.build())".format(LIB_PATH))
+        h = ctypes.CDLL(LIB_PATH)
+        vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+        h.edv_verify_batch.argtypes = [vp, vp, vp, vp, u64, vp, ctypes.c_uint32]
+        h.edv_verify_batch.restype = ctypes.c_int
+        h.edv_verify_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, vp]
+        h.edv_verify_batch_dev.restype = ctypes.c_int
+        h.edv_time_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_float)]
+        h.edv_time_batch_dev.restype = ctypes.c_int
+        h.edv_device_count.argtypes = []
+        h.edv_device_count.restype = ctypes.c_int
+        h.edv_dev_alloc.argtypes = [ctypes.c_int, u64, ctypes.POINTER(ctypes.c_void_p)]
+        h.edv_dev_free.argtypes = [ctypes.c_int, vp]
+        h.edv_h2d.argtypes = [ctypes.c_int, vp, vp, u64]
+        h.edv_d2h.argtypes = [ctypes.c_int, vp, vp, u64]
+        h.edv_version.restype = ctypes.c_char_p
+        h.edv_last_error.restype = ctypes.c_char_p
+        _lib = h
+        return h
+
+
+def version() -> str:
+    return lib().edv_version().decode()
+
+
+def device_count() -> int:
+    return lib().edv_device_count()
+
+
+def _check(rc):
+    if rc != EDV_OK:
+        what = lib().edv_last_error().decode(errors="replace")
+        if rc == EDV_E_NODEV:
+            raise EdvUnavailable(what)
+        raise EdvError(rc, what)
+
+
+def verify_arrays(sigs, pks, msgs, offsets, device_mask: int = 0) -> np.ndarray:
+    """Verify n detached 64-byte signatures laid out as the C-ABI expects.
+
+    sigs: n*64 bytes, pks: n*32 bytes, msgs: concatenated messages, offsets:
+    n+1 uint64 byte offsets.  Returns a uint8 array of n verdicts (1 = accept),
+    bit-exact with libsodium crypto_sign_ed25519_verify_detached.
+    """
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(off) - 1
+    if n <= 0:
+        return np.zeros(0, dtype=np.uint8)
+    sigs = np.frombuffer(bytes(sigs), dtype=np.uint8) if not isinstance(sigs, np.ndarray) else sigs
+    pks = np.frombuffer(bytes(pks), dtype=np.uint8) if not isinstance(pks, np.ndarray) else pks
+    if not isinstance(msgs, np.ndarray):
+        msgs = np.frombuffer(bytes(msgs) or b"\0", dtype=np.uint8)
+    if sigs.nbytes != 64 * n or pks.nbytes != 32 * n:
+        raise ValueError("sigs/pks size does not match offsets")
+    if int(off[-1]) > msgs.nbytes:
+        raise ValueError("offsets exceed the message buffer")
+    accept = np.zeros(n, dtype=np.uint8)
+    _check(lib().edv_verify_batch(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, off.ctypes.data, n,
+                                  accept.ctypes.data, device_mask))
+    return accept
+
+
+def verify_detached_batch(items, device_mask: int = 0):
+    """items: iterable of (sig64: bytes, msg: bytes, pk32: bytes) -> list[bool]."""
+    items = list(items)
+    if not items:
+        return []
+    for s, _m, p in items:
+        if len(s) != 64 or len(p) != 32:
+            raise ValueError("verify_detached_batch needs 64-byte sigs and 32-byte keys")
+    off = np.zeros(len(items) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(m) for _s, m, _p in items])
+    acc = verify_arrays(b"".join(s for s, _m, _p in items), b"".join(p for _s, _m, p in items),
+                        b"".join(m for _s, m, _p in items), off, device_mask)
+    return [bool(a) for a in acc]
+
+
+def open_batch(items, device_mask: int = 0):
+    """crypto_sign_open semantics on (signature, msg, pk) triples, batched.
+
+    Mirrors nacl_wrappers.Verifier.verify (nacl_wrappers.py:232-242): the signed
+    message is signature + msg and libsodium splits it positionally, so a
+    signature of any length is accepted iff (sm[:64], sm[64:]) verifies; sm
+    shorter than 64 bytes rejects without reaching the GPU.  pk must be 32 bytes.
+    """
+    items = list(items)
+    out = [False] * len(items)
+    todo = []
+    idx = []
+    for k, (sig, msg, pk) in enumerate(items):
+        if len(pk) != 32:
+            raise ValueError("public key must be 32 bytes")
+        if len(sig) == 64:
+            todo.append((sig, msg, pk))
+        else:
+            sm = bytes(sig) + bytes(msg)
+            if len(sm) < 64:
+                continue
+            todo.append((sm[:64], sm[64:], pk))
+        idx.append(k)
+    if todo:
+        for k, ok in zip(idx, verify_detached_batch(todo, device_mask)):
+            out[k] = ok
+    return out
+
+
+class DeviceBuffer:
+    """A raw device allocation through the C-ABI (no PyTorch needed)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        self.device = device
+        self.nbytes = nbytes
+        p = ctypes.c_void_p()
+        _check(lib().edv_dev_alloc(device, nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+
+    def upload(self, host):
+        a = np.ascontiguousarray(host)
+        assert a.nbytes <= self.nbytes
+        _check(lib().edv_h2d(self.device, self.ptr, a.ctypes.data, a.nbytes))
+
+    def download(self, nbytes=None, dtype=np.uint8):
+        nbytes = self.nbytes if nbytes is None else nbytes
+        out = np.empty(nbytes, dtype=np.uint8)
+        _check(lib().edv_d2h(self.device, out.ctypes.data, self.ptr, nbytes))
+        return out.view(dtype)
+
+    def free(self):
+        if self.ptr:
+            lib().edv_dev_free(self.device, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def verify_device(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, msg_base=0, stream=None):
+    """Device-resident verify (pointers are ints); async on `stream` if given."""
+    _check(lib().edv_verify_batch_dev(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, stream))
+
+
+def time_device(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, iters=1, msg_base=0) -> float:
+    """Milliseconds for `iters` back-to-back kernel launches (HIP events on the kernel's stream)."""
+    ms = ctypes.c_float(0)
+    _check(lib().edv_time_batch_dev(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, iters,
+                                    ctypes.byref(ms)))
+    return float(ms.value)

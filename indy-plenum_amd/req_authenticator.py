@@ -1,0 +1,102 @@
+"""ReqAuthenticator (plenum/server/req_authenticator.py:11-55) plus
+authenticate_batch, the entry point a Node's client-inbox batch goes through
+(SURVEY.md section 8b).
+
+authenticate_batch(reqs) returns, for each request, exactly what
+authenticate(req) returns or raises (the exception instance in place of a
+raise): query short-circuit, registration order, deepcopy per authenticator,
+union of identifiers, NoAuthenticatorFound.  Authenticators are applied in
+order; each batch-capable one (authenticate_batch) sees all requests still
+alive at its position in one call, i.e. one GPU launch per authenticator.
+"""
+from copy import deepcopy
+from typing import Optional
+
+from .client_authn import ClientAuthNr
+from .constants import OPERATION, TXN_TYPE
+from .exceptions import NoAuthenticatorFound
+
+
+class ReqAuthenticator:
+    """Ordered list of authenticators; the first one is the core authenticator."""
+
+    def __init__(self):
+        self._authenticators = []
+
+    def register_authenticator(self, authenticator: ClientAuthNr):
+        self._authenticators.append(authenticator)
+
+    def authenticate(self, req_data):
+        identifiers = set()
+        typ = req_data.get(OPERATION, {}).get(TXN_TYPE)
+        for authenticator in self._authenticators:
+            if authenticator.is_query(typ):
+                return set()
+            if not (authenticator.is_write(typ) or authenticator.is_action(typ)):
+                continue
+            rv = authenticator.authenticate(deepcopy(req_data)) or set()
+            identifiers.update(rv)
+        if not identifiers:
+            raise NoAuthenticatorFound
+        return identifiers
+
+    def authenticate_batch(self, reqs):
+        n = len(reqs)
+        out = [None] * n
+        idents = [set() for _ in range(n)]
+        alive = []  # requests still being processed (no result yet)
+        typs = []
+        for k, req in enumerate(reqs):
+            try:
+                typs.append(req.get(OPERATION, {}).get(TXN_TYPE))
+            except Exception as ex:  # malformed operation: authenticate() would raise the same
+                typs.append(None)
+                out[k] = ex
+                continue
+            alive.append(k)
+        for authenticator in self._authenticators:
+            if not alive:
+                break
+            todo = []
+            still = []
+            for k in alive:
+                if authenticator.is_query(typs[k]):
+                    out[k] = set()
+                    continue
+                still.append(k)
+                if authenticator.is_write(typs[k]) or authenticator.is_action(typs[k]):
+                    todo.append(k)
+            alive = still
+            if not todo:
+                continue
+            if hasattr(authenticator, "authenticate_batch"):
+                results = authenticator.authenticate_batch([deepcopy(reqs[k]) for k in todo])
+            else:
+                results = []
+                for k in todo:
+                    try:
+                        results.append(authenticator.authenticate(deepcopy(reqs[k])))
+                    except Exception as ex:
+                        results.append(ex)
+            failed = set()
+            for k, rv in zip(todo, results):
+                if isinstance(rv, BaseException):
+                    out[k] = rv
+                    failed.add(k)
+                else:
+                    idents[k].update(rv or set())
+            alive = [k for k in alive if k not in failed]
+        for k in alive:
+            out[k] = idents[k] if idents[k] else NoAuthenticatorFound()
+        return out
+
+    @property
+    def core_authenticator(self):
+        if not self._authenticators:
+            raise RuntimeError('No authenticator registered yet')
+        return self._authenticators[0]
+
+    def get_authnr_by_type(self, authnr_type) -> Optional[ClientAuthNr]:
+        for authnr in self._authenticators:
+            if isinstance(authnr, authnr_type):
+                return authnr

@@ -1,0 +1,599 @@
+/*
+ * ed25519_oracle.c -- TEST INFRASTRUCTURE ONLY (the parity checker).
+ *
+ * A plain-C restatement of the verdict the reference computes on its client
+ * request authentication path:
+ *
+ *   plenum/common/verifier.py:54-55          DidVerifier.verify -> NaclVerifier.verify
+ *   stp_core/crypto/nacl_wrappers.py:232-242 Verifier.verify: crypto_sign_open(sig + msg, pk)
+ *   stp_core/crypto/nacl_wrappers.py:86-108  VerifyKey.verify -> libnacl.crypto_sign_open
+ *
+ * The arithmetic lives in the third-party dependency libsodium (reached through
+ * libnacl==1.6.1, setup.py:49).  Its source is not in /root/reference; the
+ * in-container binary is libsodium 1.0.18 (/opt/conda/lib/libsodium.so.23).
+ * This file restates the published algorithm of libsodium 1.0.18
+ * crypto_sign_ed25519_verify_detached (RFC 8032 Ed25519 with libsodium's
+ * strictness rules):
+ *
+ *   V2  if (sig[63] & 0xF0) and S >= L             -> reject
+ *   V3  R in the 7-entry small-order blocklist     -> reject (sign bit masked)
+ *   V4  A non-canonical (y >= p) or small order    -> reject
+ *   V5  decompress A (negated); off curve          -> reject
+ *   V6  h = SHA-512(R || A || M), A bytes as given
+ *   V7  h mod L
+ *   V8  R' = [h](-A) + [S]B        (cofactorless)
+ *   V9  accept iff encode(R') == R (32-byte compare)
+ *
+ * Parity of this restatement is PINNED by tests/golden/ed25519_golden.bin
+ * (verdicts produced by libsodium 1.0.18 itself, tests/golden/make_golden.py)
+ * and by the reference's own fixtures KAT-1/KAT-2.
+ *
+ * Nothing in the product path may link or call this file: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg use it, as the
+ * checker.  It also carries the deterministic corpus generator (signing),
+ * because the GPU box has no libsodium guarantee and must regenerate the
+ * parity corpus from a seed.
+ *
+ * Representation: GF(2^255-19) in 5 x 51-bit limbs with 128-bit products;
+ * points in extended twisted-Edwards coordinates (X:Y:Z:T), a = -1, with the
+ * unified (complete) addition law, so torsion and mixed-order inputs need no
+ * special cases.  Scalar multiplication is plain double-and-add: slow and
+ * obviously correct.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+
+typedef unsigned __int128 u128;
+typedef struct { uint64_t v[5]; } fe;
+typedef struct { fe X, Y, Z, T; } ge;
+
+#define MASK51 ((1ULL << 51) - 1)
+
+/* ------------------------------------------------------------------ SHA-512 */
+static const uint64_t K512[80] = {
+  0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+  0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+  0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+  0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+  0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+  0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+  0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+  0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+  0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+  0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+  0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+  0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+  0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+  0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+  0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+  0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+  0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+  0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+  0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+  0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+static uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+static uint64_t be64(const uint8_t *p) {
+  uint64_t r = 0;
+  for (int i = 0; i < 8; i++) r = (r << 8) | p[i];
+  return r;
+}
+
+static void sha512_block(uint64_t H[8], const uint8_t *blk) {
+  uint64_t W[80], a, b, c, d, e, f, g, h;
+  for (int t = 0; t < 16; t++) W[t] = be64(blk + 8 * t);
+  for (int t = 16; t < 80; t++) {
+    uint64_t s0 = rotr64(W[t - 15], 1) ^ rotr64(W[t - 15], 8) ^ (W[t - 15] >> 7);
+    uint64_t s1 = rotr64(W[t - 2], 19) ^ rotr64(W[t - 2], 61) ^ (W[t - 2] >> 6);
+    W[t] = W[t - 16] + s0 + W[t - 7] + s1;
+  }
+  a = H[0]; b = H[1]; c = H[2]; d = H[3]; e = H[4]; f = H[5]; g = H[6]; h = H[7];
+  for (int t = 0; t < 80; t++) {
+    uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+    uint64_t ch = (e & f) ^ (~e & g);
+    uint64_t t1 = h + S1 + ch + K512[t] + W[t];
+    uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+    uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint64_t t2 = S0 + mj;
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+}
+
+/* SHA-512 over the concatenation of up to 3 byte strings (R || A || M). */
+static void sha512_3(uint8_t out[64], const uint8_t *p0, size_t n0, const uint8_t *p1, size_t n1,
+                     const uint8_t *p2, size_t n2) {
+  uint64_t H[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                   0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                   0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  uint8_t blk[128];
+  size_t fill = 0;
+  uint64_t total = (uint64_t)n0 + n1 + n2;
+  const uint8_t *ps[3] = {p0, p1, p2};
+  size_t ns[3] = {n0, n1, n2};
+  for (int s = 0; s < 3; s++) {
+    const uint8_t *p = ps[s];
+    size_t n = ns[s];
+    while (n) {
+      size_t take = 128 - fill < n ? 128 - fill : n;
+      memcpy(blk + fill, p, take);
+      fill += take; p += take; n -= take;
+      if (fill == 128) { sha512_block(H, blk); fill = 0; }
+    }
+  }
+  blk[fill++] = 0x80;
+  if (fill > 112) { memset(blk + fill, 0, 128 - fill); sha512_block(H, blk); fill = 0; }
+  memset(blk + fill, 0, 128 - fill);
+  /* 128-bit big-endian bit length in bytes 112..127 */
+  uint64_t bits_lo = total << 3, bits_hi = total >> 61;
+  for (int i = 0; i < 8; i++) {
+    blk[127 - i] = (uint8_t)(bits_lo >> (8 * i));
+    blk[119 - i] = (uint8_t)(bits_hi >> (8 * i));
+  }
+  sha512_block(H, blk);
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 8; j++) out[8 * i + j] = (uint8_t)(H[i] >> (56 - 8 * j));
+}
+
+void oref_sha512(uint8_t out[64], const uint8_t *m, uint64_t n) { sha512_3(out, m, n, 0, 0, 0, 0); }
+
+/* ------------------------------------------------------------ GF(2^255-19) */
+static void fe_0(fe *h) { memset(h, 0, sizeof *h); }
+static void fe_1(fe *h) { fe_0(h); h->v[0] = 1; }
+
+static void fe_carry(fe *h) {
+  uint64_t c;
+  for (int k = 0; k < 2; k++) {
+    c = h->v[0] >> 51; h->v[0] &= MASK51; h->v[1] += c;
+    c = h->v[1] >> 51; h->v[1] &= MASK51; h->v[2] += c;
+    c = h->v[2] >> 51; h->v[2] &= MASK51; h->v[3] += c;
+    c = h->v[3] >> 51; h->v[3] &= MASK51; h->v[4] += c;
+    c = h->v[4] >> 51; h->v[4] &= MASK51; h->v[0] += 19 * c;
+  }
+}
+static void fe_add(fe *h, const fe *f, const fe *g) {
+  for (int i = 0; i < 5; i++) h->v[i] = f->v[i] + g->v[i];
+  fe_carry(h);
+}
+/* f - g computed as f + 4p - g: inputs are carried (< 2^52) so no underflow. */
+static void fe_sub(fe *h, const fe *f, const fe *g) {
+  static const uint64_t fourp[5] = {0x1FFFFFFFFFFFB4ULL, 0x1FFFFFFFFFFFFCULL, 0x1FFFFFFFFFFFFCULL,
+                                     0x1FFFFFFFFFFFFCULL, 0x1FFFFFFFFFFFFCULL};
+  for (int i = 0; i < 5; i++) h->v[i] = f->v[i] + fourp[i] - g->v[i];
+  fe_carry(h);
+}
+static void fe_neg(fe *h, const fe *f) { fe z; fe_0(&z); fe_sub(h, &z, f); }
+static void fe_mul(fe *h, const fe *f, const fe *g) {
+  const uint64_t *a = f->v, *b = g->v;
+  u128 r[5] = {0, 0, 0, 0, 0};
+  for (int i = 0; i < 5; i++)
+    for (int j = 0; j < 5; j++) {
+      u128 p = (u128)a[i] * b[j];
+      if (i + j < 5) r[i + j] += p;
+      else r[i + j - 5] += p * 19;
+    }
+  uint64_t c = 0;
+  for (int i = 0; i < 5; i++) {
+    r[i] += c;
+    h->v[i] = (uint64_t)r[i] & MASK51;
+    c = (uint64_t)(r[i] >> 51);
+  }
+  h->v[0] += 19 * c;
+  fe_carry(h);
+}
+static void fe_sq(fe *h, const fe *f) { fe_mul(h, f, f); }
+
+static void fe_frombytes(fe *h, const uint8_t s[32]) {
+  /* 255 low bits; the sign bit (bit 255) is ignored; the value may be >= p. */
+  uint64_t w[4];
+  for (int i = 0; i < 4; i++) {
+    w[i] = 0;
+    for (int j = 7; j >= 0; j--) w[i] = (w[i] << 8) | s[8 * i + j];
+  }
+  h->v[0] = w[0] & MASK51;
+  h->v[1] = ((w[0] >> 51) | (w[1] << 13)) & MASK51;
+  h->v[2] = ((w[1] >> 38) | (w[2] << 26)) & MASK51;
+  h->v[3] = ((w[2] >> 25) | (w[3] << 39)) & MASK51;
+  h->v[4] = (w[3] >> 12) & MASK51;
+}
+static void fe_tobytes(uint8_t s[32], const fe *f) {
+  fe t = *f;
+  fe_carry(&t);
+  /* t < 2^255 + small; subtract p if t >= p (constant-free version: add 19, check bit 255) */
+  uint64_t q = (t.v[0] + 19) >> 51;
+  q = (t.v[1] + q) >> 51;
+  q = (t.v[2] + q) >> 51;
+  q = (t.v[3] + q) >> 51;
+  q = (t.v[4] + q) >> 51;
+  t.v[0] += 19 * q;
+  uint64_t c;
+  c = t.v[0] >> 51; t.v[0] &= MASK51; t.v[1] += c;
+  c = t.v[1] >> 51; t.v[1] &= MASK51; t.v[2] += c;
+  c = t.v[2] >> 51; t.v[2] &= MASK51; t.v[3] += c;
+  c = t.v[3] >> 51; t.v[3] &= MASK51; t.v[4] += c;
+  t.v[4] &= MASK51;
+  uint64_t w[4];
+  w[0] = t.v[0] | (t.v[1] << 51);
+  w[1] = (t.v[1] >> 13) | (t.v[2] << 38);
+  w[2] = (t.v[2] >> 26) | (t.v[3] << 25);
+  w[3] = (t.v[3] >> 39) | (t.v[4] << 12);
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 8; j++) s[8 * i + j] = (uint8_t)(w[i] >> (8 * j));
+}
+static int fe_iszero(const fe *f) {
+  uint8_t s[32], d = 0;
+  fe_tobytes(s, f);
+  for (int i = 0; i < 32; i++) d |= s[i];
+  return d == 0;
+}
+static int fe_isnegative(const fe *f) {
+  uint8_t s[32];
+  fe_tobytes(s, f);
+  return s[0] & 1;
+}
+/* f^e for a 255-bit exponent given little-endian bytes (square-and-multiply). */
+static void fe_pow(fe *h, const fe *f, const uint8_t e[32]) {
+  fe r, b = *f;
+  fe_1(&r);
+  for (int i = 255; i >= 0; i--) {
+    fe_sq(&r, &r);
+    if ((e[i >> 3] >> (i & 7)) & 1) fe_mul(&r, &r, &b);
+  }
+  *h = r;
+}
+/* exponents: p-2 and (p-5)/8 */
+static uint8_t E_PM2[32], E_P58[32];
+static fe FE_D, FE_D2, FE_SQRTM1;
+static ge GE_B;
+static int g_inited;
+
+static void fe_invert(fe *h, const fe *f) { fe_pow(h, f, E_PM2); }
+static void fe_pow22523(fe *h, const fe *f) { fe_pow(h, f, E_P58); }
+
+/* ------------------------------------------------------------- the group */
+static void ge_identity(ge *p) { fe_0(&p->X); fe_1(&p->Y); fe_1(&p->Z); fe_0(&p->T); }
+
+/* unified addition, extended coordinates, a = -1 (add-2008-hwcd-3) */
+static void ge_add(ge *r, const ge *p, const ge *q) {
+  fe a, b, c, d, e, f, g, h, t1, t2;
+  fe_sub(&t1, &p->Y, &p->X); fe_sub(&t2, &q->Y, &q->X); fe_mul(&a, &t1, &t2);
+  fe_add(&t1, &p->Y, &p->X); fe_add(&t2, &q->Y, &q->X); fe_mul(&b, &t1, &t2);
+  fe_mul(&c, &p->T, &q->T); fe_mul(&c, &c, &FE_D2);
+  fe_mul(&d, &p->Z, &q->Z); fe_add(&d, &d, &d);
+  fe_sub(&e, &b, &a); fe_sub(&f, &d, &c); fe_add(&g, &d, &c); fe_add(&h, &b, &a);
+  fe_mul(&r->X, &e, &f); fe_mul(&r->Y, &g, &h); fe_mul(&r->T, &e, &h); fe_mul(&r->Z, &f, &g);
+}
+/* doubling, a = -1 (dbl-2008-hwcd) */
+static void ge_dbl(ge *r, const ge *p) {
+  fe a, b, c, d, e, g, f, h, t;
+  fe_sq(&a, &p->X); fe_sq(&b, &p->Y); fe_sq(&c, &p->Z); fe_add(&c, &c, &c);
+  fe_neg(&d, &a);
+  fe_add(&t, &p->X, &p->Y); fe_sq(&e, &t); fe_sub(&e, &e, &a); fe_sub(&e, &e, &b);
+  fe_add(&g, &d, &b); fe_sub(&f, &g, &c); fe_sub(&h, &d, &b);
+  fe_mul(&r->X, &e, &f); fe_mul(&r->Y, &g, &h); fe_mul(&r->T, &e, &h); fe_mul(&r->Z, &f, &g);
+}
+static void ge_tobytes(uint8_t s[32], const ge *p) {
+  fe zi, x, y;
+  fe_invert(&zi, &p->Z);
+  fe_mul(&x, &p->X, &zi);
+  fe_mul(&y, &p->Y, &zi);
+  fe_tobytes(s, &y);
+  s[31] ^= (uint8_t)(fe_isnegative(&x) << 7);
+}
+/* libsodium ge25519_frombytes_negate_vartime: decode s and negate x. */
+static int ge_frombytes_negate(ge *h, const uint8_t s[32]) {
+  fe u, v, v3, vxx, chk, one;
+  fe_1(&one);
+  fe_frombytes(&h->Y, s);
+  fe_1(&h->Z);
+  fe_sq(&u, &h->Y);
+  fe_mul(&v, &u, &FE_D);
+  fe_sub(&u, &u, &one);  /* y^2 - 1 */
+  fe_add(&v, &v, &one);  /* d y^2 + 1 */
+  fe_sq(&v3, &v); fe_mul(&v3, &v3, &v);
+  fe_sq(&h->X, &v3); fe_mul(&h->X, &h->X, &v); fe_mul(&h->X, &h->X, &u);
+  fe_pow22523(&h->X, &h->X);
+  fe_mul(&h->X, &h->X, &v3); fe_mul(&h->X, &h->X, &u);
+  fe_sq(&vxx, &h->X); fe_mul(&vxx, &vxx, &v);
+  fe_sub(&chk, &vxx, &u);
+  if (!fe_iszero(&chk)) {
+    fe_add(&chk, &vxx, &u);
+    if (!fe_iszero(&chk)) return -1;
+    fe_mul(&h->X, &h->X, &FE_SQRTM1);
+  }
+  if (fe_isnegative(&h->X) == (s[31] >> 7)) fe_neg(&h->X, &h->X);
+  fe_mul(&h->T, &h->X, &h->Y);
+  return 0;
+}
+/* [k]P, double-and-add from the top bit (k little-endian, 256 bits). */
+static void ge_scalarmult(ge *r, const uint8_t k[32], const ge *p) {
+  ge acc;
+  ge_identity(&acc);
+  for (int i = 255; i >= 0; i--) {
+    ge_dbl(&acc, &acc);
+    if ((k[i >> 3] >> (i & 7)) & 1) ge_add(&acc, &acc, p);
+  }
+  *r = acc;
+}
+
+/* ---------------------------------------------------------------- scalars */
+/* L = 2^252 + 27742317777372353535851937790883648493, little-endian bytes */
+static const uint8_t L_BYTES[32] = {0xed, 0xd3, 0xf5, 0x5c, 0x1a, 0x63, 0x12, 0x58, 0xd6, 0x9c, 0xf7,
+                                    0xa2, 0xde, 0xf9, 0xde, 0x14, 0,    0,    0,    0,    0,    0,
+                                    0,    0,    0,    0,    0,    0,    0,    0,    0,    0x10};
+
+/* big numbers as 9 x 32-bit words (288 bits) for the bit-serial reduction */
+static int bn_geq(const uint32_t *a, const uint32_t *b, int n) {
+  for (int i = n - 1; i >= 0; i--) {
+    if (a[i] != b[i]) return a[i] > b[i];
+  }
+  return 1;
+}
+static void bn_sub(uint32_t *a, const uint32_t *b, int n) {
+  uint64_t br = 0;
+  for (int i = 0; i < n; i++) {
+    uint64_t d = (uint64_t)a[i] - b[i] - br;
+    a[i] = (uint32_t)d;
+    br = (d >> 63) & 1;
+  }
+}
+/* r = x mod L where x is nbytes little-endian (bit-serial shift/subtract) */
+static void sc_mod(uint8_t r[32], const uint8_t *x, int nbytes) {
+  uint32_t acc[9] = {0}, L[9] = {0};
+  for (int i = 0; i < 32; i++) L[i / 4] |= (uint32_t)L_BYTES[i] << (8 * (i % 4));
+  for (int bit = nbytes * 8 - 1; bit >= 0; bit--) {
+    for (int i = 8; i > 0; i--) acc[i] = (acc[i] << 1) | (acc[i - 1] >> 31);
+    acc[0] = (acc[0] << 1) | ((x[bit >> 3] >> (bit & 7)) & 1);
+    if (bn_geq(acc, L, 9)) bn_sub(acc, L, 9);
+  }
+  for (int i = 0; i < 32; i++) r[i] = (uint8_t)(acc[i / 4] >> (8 * (i % 4)));
+}
+/* r = (a*b + c) mod L */
+static void sc_muladd(uint8_t r[32], const uint8_t a[32], const uint8_t b[32], const uint8_t c[32]) {
+  uint32_t prod[17] = {0};
+  for (int i = 0; i < 8; i++) {
+    uint64_t carry = 0;
+    uint32_t ai = (uint32_t)a[4 * i] | (uint32_t)a[4 * i + 1] << 8 | (uint32_t)a[4 * i + 2] << 16 |
+                  (uint32_t)a[4 * i + 3] << 24;
+    for (int j = 0; j < 8; j++) {
+      uint32_t bj = (uint32_t)b[4 * j] | (uint32_t)b[4 * j + 1] << 8 | (uint32_t)b[4 * j + 2] << 16 |
+                    (uint32_t)b[4 * j + 3] << 24;
+      uint64_t t = (uint64_t)ai * bj + prod[i + j] + carry;
+      prod[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    prod[i + 8] += (uint32_t)carry;
+  }
+  uint64_t carry = 0;
+  for (int i = 0; i < 17; i++) {
+    uint32_t ci = i < 8 ? ((uint32_t)c[4 * i] | (uint32_t)c[4 * i + 1] << 8 | (uint32_t)c[4 * i + 2] << 16 |
+                           (uint32_t)c[4 * i + 3] << 24)
+                        : 0;
+    uint64_t t = (uint64_t)prod[i] + ci + carry;
+    prod[i] = (uint32_t)t;
+    carry = t >> 32;
+  }
+  uint8_t bytes[68];
+  for (int i = 0; i < 17; i++)
+    for (int j = 0; j < 4; j++) bytes[4 * i + j] = (uint8_t)(prod[i] >> (8 * j));
+  sc_mod(r, bytes, 68);
+}
+/* libsodium sc25519_is_canonical: S < L */
+static int sc_is_canonical(const uint8_t s[32]) {
+  for (int i = 31; i >= 0; i--) {
+    if (s[i] != L_BYTES[i]) return s[i] < L_BYTES[i];
+  }
+  return 0;
+}
+
+/* ------------------------------------------------- libsodium strictness */
+/* ge25519_has_small_order: the 7-entry blocklist, sign bit masked */
+static const uint8_t BLOCKLIST[7][32] = {
+  /* 0 (order 4) */
+  {0},
+  /* 1 (order 1) */
+  {1},
+  /* order 8 */
+  {0x26, 0xe8, 0x95, 0x8f, 0xc2, 0xb2, 0x27, 0xb0, 0x45, 0xc3, 0xf4, 0x89, 0xf2, 0xef, 0x98, 0xf0,
+   0xd5, 0xdf, 0xac, 0x05, 0xd3, 0xc6, 0x33, 0x39, 0xb1, 0x38, 0x02, 0x88, 0x6d, 0x53, 0xfc, 0x05},
+  /* order 8 */
+  {0xc7, 0x17, 0x6a, 0x70, 0x3d, 0x4d, 0xd8, 0x4f, 0xba, 0x3c, 0x0b, 0x76, 0x0d, 0x10, 0x67, 0x0f,
+   0x2a, 0x20, 0x53, 0xfa, 0x2c, 0x39, 0xcc, 0xc6, 0x4e, 0xc7, 0xfd, 0x77, 0x92, 0xac, 0x03, 0x7a},
+  /* p-1 (order 2) */
+  {0xec, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+   0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0x7f},
+  /* p (= 0, order 4) */
+  {0xed, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+   0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0x7f},
+  /* p+1 (= 1, order 1) */
+  {0xee, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+   0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0x7f}};
+
+static int has_small_order(const uint8_t s[32]) {
+  for (int k = 0; k < 7; k++) {
+    int eq = 1;
+    for (int j = 0; j < 31; j++) eq &= s[j] == BLOCKLIST[k][j];
+    eq &= (s[31] & 0x7f) == BLOCKLIST[k][31];
+    if (eq) return 1;
+  }
+  return 0;
+}
+/* ge25519_is_canonical: the low 255 bits encode y < p */
+static int ge_is_canonical(const uint8_t s[32]) {
+  if ((s[31] & 0x7f) != 0x7f) return 1;
+  for (int i = 30; i > 0; i--)
+    if (s[i] != 0xff) return 1;
+  return s[0] < 0xed;
+}
+
+/* ------------------------------------------------------------------ init */
+static void oref_init_once(void) {
+  if (g_inited) return;
+  /* p-2 and (p-5)/8 as little-endian bytes */
+  memset(E_PM2, 0xff, 32); E_PM2[0] = 0xeb; E_PM2[31] = 0x7f;
+  memset(E_P58, 0xff, 32); E_P58[0] = 0xfd; E_P58[31] = 0x0f;
+  fe a, b, t;
+  fe_0(&a); a.v[0] = 121665; fe_neg(&a, &a);
+  fe_0(&b); b.v[0] = 121666; fe_invert(&t, &b);
+  fe_mul(&FE_D, &a, &t);
+  fe_add(&FE_D2, &FE_D, &FE_D);
+  /* sqrt(-1) = 2^((p-1)/4) */
+  uint8_t e[32];
+  memset(e, 0xff, 32); e[0] = 0xfb; e[31] = 0x1f;
+  fe two; fe_0(&two); two.v[0] = 2;
+  fe_pow(&FE_SQRTM1, &two, e);
+  /* B: y = 4/5, x even.  Decode the canonical encoding with the negating decoder, then negate back. */
+  fe four, five, y;
+  fe_0(&four); four.v[0] = 4; fe_0(&five); five.v[0] = 5;
+  fe_invert(&t, &five); fe_mul(&y, &four, &t);
+  uint8_t by[32];
+  fe_tobytes(by, &y);
+  ge nb;
+  ge_frombytes_negate(&nb, by);
+  fe_neg(&GE_B.X, &nb.X); GE_B.Y = nb.Y; GE_B.Z = nb.Z; fe_neg(&GE_B.T, &nb.T);
+  g_inited = 1;
+}
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+static void oref_init(void) { pthread_once(&g_once, oref_init_once); }
+
+/* ---------------------------------------------------------- public: verify */
+/* Restates libsodium 1.0.18 crypto_sign_ed25519_verify_detached: 0 accept, -1 reject. */
+int oref_verify_detached(const uint8_t sig[64], const uint8_t *m, uint64_t mlen, const uint8_t pk[32]) {
+  oref_init();
+  if ((sig[63] & 0xF0) && !sc_is_canonical(sig + 32)) return -1;        /* V2 */
+  if (has_small_order(sig)) return -1;                                   /* V3 */
+  if (!ge_is_canonical(pk) || has_small_order(pk)) return -1;            /* V4 */
+  ge negA;
+  if (ge_frombytes_negate(&negA, pk) != 0) return -1;                    /* V5 */
+  uint8_t h[64], hr[32];
+  sha512_3(h, sig, 32, pk, 32, m, (size_t)mlen);                         /* V6 */
+  sc_mod(hr, h, 64);                                                     /* V7 */
+  ge t1, t2, r;
+  ge_scalarmult(&t1, hr, &negA);                                         /* V8 */
+  ge_scalarmult(&t2, sig + 32, &GE_B);
+  ge_add(&r, &t1, &t2);
+  uint8_t rc[32];
+  ge_tobytes(rc, &r);                                                    /* V9 */
+  return memcmp(rc, sig, 32) == 0 ? 0 : -1;
+}
+
+/* crypto_sign_open semantics on sm = sig || M (positional split; smlen < 64 rejects) */
+int oref_sign_open(const uint8_t *sm, uint64_t smlen, const uint8_t pk[32]) {
+  if (smlen < 64) return -1;
+  return oref_verify_detached(sm, sm + 64, smlen - 64, pk);
+}
+
+/* ------------------------------------------------------ public: signing */
+/* Fixed-base comb for the generator: TB[i][j] = j * 16^i * B (i < 64, j < 16). */
+static ge TB[64][16];
+static pthread_once_t g_tb_once = PTHREAD_ONCE_INIT;
+static void tb_init(void) {
+  oref_init();
+  ge base = GE_B;
+  for (int i = 0; i < 64; i++) {
+    ge_identity(&TB[i][0]);
+    for (int j = 1; j < 16; j++) ge_add(&TB[i][j], &TB[i][j - 1], &base);
+    for (int k = 0; k < 4; k++) ge_dbl(&base, &base);
+  }
+}
+static void ge_scalarmult_base(ge *r, const uint8_t k[32]) {
+  pthread_once(&g_tb_once, tb_init);
+  ge acc;
+  ge_identity(&acc);
+  for (int i = 0; i < 64; i++) {
+    int nib = (k[i >> 1] >> (4 * (i & 1))) & 15;
+    ge_add(&acc, &acc, &TB[i][nib]);
+  }
+  *r = acc;
+}
+
+void oref_seed_keypair(uint8_t pk[32], uint8_t sk[64], const uint8_t seed[32]) {
+  oref_init();
+  uint8_t h[64];
+  sha512_3(h, seed, 32, 0, 0, 0, 0);
+  h[0] &= 248; h[31] &= 127; h[31] |= 64;
+  ge A;
+  ge_scalarmult_base(&A, h);
+  ge_tobytes(pk, &A);
+  memcpy(sk, seed, 32);
+  memcpy(sk + 32, pk, 32);
+}
+
+/* RFC 8032 / libsodium crypto_sign_detached (deterministic) */
+void oref_sign_detached(uint8_t sig[64], const uint8_t *m, uint64_t mlen, const uint8_t sk[64]) {
+  oref_init();
+  uint8_t az[64], nonce[64], r[32], hram[64], h[32];
+  sha512_3(az, sk, 32, 0, 0, 0, 0);
+  az[0] &= 248; az[31] &= 127; az[31] |= 64;
+  sha512_3(nonce, az + 32, 32, m, (size_t)mlen, 0, 0);
+  sc_mod(r, nonce, 64);
+  ge R;
+  ge_scalarmult_base(&R, r);
+  ge_tobytes(sig, &R);
+  sha512_3(hram, sig, 32, sk + 32, 32, m, (size_t)mlen);
+  sc_mod(h, hram, 64);
+  sc_muladd(sig + 32, h, az, r);
+}
+
+/* component oracles used by the unit tests */
+void oref_sc_reduce64(uint8_t r[32], const uint8_t s[64]) { sc_mod(r, s, 64); }
+int oref_has_small_order(const uint8_t s[32]) { return has_small_order(s); }
+int oref_ge_is_canonical(const uint8_t s[32]) { return ge_is_canonical(s); }
+int oref_sc_is_canonical(const uint8_t s[32]) { return sc_is_canonical(s); }
+/* encode(P1 + P2) for encoded inputs; returns -1 if either fails to decode */
+int oref_point_add(uint8_t out[32], const uint8_t p[32], const uint8_t q[32]) {
+  oref_init();
+  ge a, b, r;
+  if (ge_frombytes_negate(&a, p) || ge_frombytes_negate(&b, q)) return -1;
+  ge_add(&r, &a, &b);
+  fe_neg(&r.X, &r.X); fe_neg(&r.T, &r.T);
+  ge_tobytes(out, &r);
+  return 0;
+}
+/* encode([k]P); k is 32 bytes little-endian, used as is (no clamping) */
+int oref_scalarmult(uint8_t out[32], const uint8_t k[32], const uint8_t p[32]) {
+  oref_init();
+  ge a, r;
+  if (ge_frombytes_negate(&a, p)) return -1;
+  fe_neg(&a.X, &a.X); fe_neg(&a.T, &a.T);
+  ge_scalarmult(&r, k, &a);
+  ge_tobytes(out, &r);
+  return 0;
+}
+void oref_scalarmult_base(uint8_t out[32], const uint8_t k[32]) {
+  ge r;
+  ge_scalarmult_base(&r, k);
+  ge_tobytes(out, &r);
+}
+
+/* ------------------------------------------------- batch verify (threads) */
+typedef struct {
+  const uint8_t *sigs, *pks, *msgs;
+  const uint64_t *off;
+  uint8_t *accept;
+  uint64_t lo, hi;
+} vjob;
+static void *vworker(void *arg) {
+  vjob *j = (vjob *)arg;
+  for (uint64_t i = j->lo; i < j->hi; i++)
+    j->accept[i] = oref_verify_detached(j->sigs + 64 * i, j->msgs + j->off[i], j->off[i + 1] - j->off[i],
+                                        j->pks + 32 * i) == 0;
+  return 0;
+}
+/* Same layout as the product C-ABI (include/edv.h); threads <= 0 means 1. */
+int oref_verify_batch(const uint8_t *sigs, const uint8_t *pks, const uint8_t *msgs, const uint64_t *off,
+                      uint64_t n, uint8_t *accept, int threads) {
+  oref_init();
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  vjob jobs[256];
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (vjob){sigs, pks, msgs, off, accept, n * t / threads, n * (t + 1) / threads};
+    if (pthread_create(&th[t], 0, vworker, &jobs[t])) return -1;
+  }
+  for (int t = 0; t < threads; t++) pthread_join(th[t], 0);
+  return 0;
+}

@@ -1,0 +1,118 @@
+"""The kernel's field/scalar/SHA-512 code and its whole per-signature algorithm,
+compiled for the CPU (libedv_hostcheck.so), against Python integers, hashlib
+and libsodium's golden verdicts.  Catches arithmetic bugs before the GPU."""
+import ctypes
+import hashlib
+import random
+
+import golden_io
+import hostcheck_lib
+
+P = 2**255 - 19
+L = 2**252 + 27742317777372353535851937790883648493
+POS = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
+# input bound the multiply is specified for: |f_i| <= 1.65 * 2^26 (even i), 1.65 * 2^25 (odd i)
+BOUND = [int(1.65 * 2**26) if i % 2 == 0 else int(1.65 * 2**25) for i in range(10)]
+
+
+def val(l):
+    return sum(int(x) << POS[i] for i, x in enumerate(l))
+
+
+def arr(l):
+    return (ctypes.c_int32 * 10)(*l)
+
+
+def limbs(x):
+    return [(x >> POS[i]) & ((1 << (26 if i % 2 == 0 else 25)) - 1) for i in range(10)]
+
+
+def rand_limbs(r, extreme=False):
+    if extreme:
+        return [r.choice([-BOUND[i], BOUND[i], BOUND[i] - 1, -BOUND[i] + 1]) for i in range(10)]
+    return [r.randrange(-BOUND[i], BOUND[i] + 1) for i in range(10)]
+
+
+def out_ok(h):
+    # outputs must be reduced enough to feed another multiply after one add/sub
+    return all(abs(h[i]) <= (2**25 + 2**20 if i % 2 == 0 else 2**24 + 2**20) for i in range(10))
+
+
+def test_fe_mul_sq_against_python():
+    hc = hostcheck_lib.load()
+    r = random.Random(5)
+    h = (ctypes.c_int32 * 10)()
+    for it in range(3000):
+        f = rand_limbs(r, extreme=(it % 3 == 0))
+        g = rand_limbs(r, extreme=(it % 5 == 0))
+        hc.hc_fe_mul(arr(f), arr(g), h)
+        assert val(h) % P == val(f) * val(g) % P and out_ok(h)
+        hc.hc_fe_sq(arr(f), h)
+        assert val(h) % P == val(f) ** 2 % P and out_ok(h)
+        hc.hc_fe_sq2(arr(f), h)
+        assert val(h) % P == 2 * val(f) ** 2 % P and out_ok(h)
+
+
+def test_fe_tobytes_canonical_and_frombytes():
+    hc = hostcheck_lib.load()
+    r = random.Random(6)
+    out = ctypes.create_string_buffer(32)
+    h = (ctypes.c_int32 * 10)()
+    specials = [0, 1, P - 1, P, P + 1, 2 * P - 1, 2**255 - 1, 2**255 - 20, 19, 2**255 - 19 - 1]
+    for x in specials + [r.randrange(2**255) for _ in range(2000)]:
+        hc.hc_fe_frombytes(x.to_bytes(32, "little"), h)
+        y = x & (2**255 - 1)  # bit 255 (the sign bit) is ignored by the decoder
+        assert val(h) % P == y % P and out_ok(h)
+        hc.hc_fe_tobytes(h, out)
+        assert int.from_bytes(out.raw, "little") == y % P
+    for _ in range(2000):  # tobytes of non-canonical reduced limb vectors
+        f = [r.randrange(-2**25, 2**25) if i % 2 == 0 else r.randrange(-2**24, 2**24) for i in range(10)]
+        hc.hc_fe_tobytes(arr(f), out)
+        assert int.from_bytes(out.raw, "little") == val(f) % P
+
+
+def test_fe_invert_and_pow22523():
+    hc = hostcheck_lib.load()
+    r = random.Random(7)
+    h = (ctypes.c_int32 * 10)()
+    for x in [1, 2, P - 1] + [r.randrange(1, P) for _ in range(30)]:
+        hc.hc_fe_invert(arr(limbs(x)), h)
+        assert val(h) % P == pow(x, P - 2, P)
+        hc.hc_fe_pow22523(arr(limbs(x)), h)
+        assert val(h) % P == pow(x, (P - 5) // 8, P)
+
+
+def test_sc_reduce_canonical():
+    hc = hostcheck_lib.load()
+    r = random.Random(8)
+    out = ctypes.create_string_buffer(32)
+    vals = [0, 1, L - 1, L, L + 1, 2 * L - 1, 2 * L, 2**512 - 1, 2**511, 2**253 - 1, 8 * L + 7]
+    vals += [k * L + d for k in (1, 2**100, 2**258 - 1) for d in (-1, 0, 1)]
+    vals += [r.randrange(2**512) for _ in range(3000)]
+    for v in vals:
+        if not 0 <= v < 2**512:
+            continue
+        hc.hc_sc_reduce(v.to_bytes(64, "little"), out)
+        assert int.from_bytes(out.raw, "little") == v % L, hex(v)
+
+
+def test_hram_sha512_all_lengths():
+    hc = hostcheck_lib.load()
+    r = random.Random(9)
+    d = ctypes.create_string_buffer(64)
+    for n in list(range(0, 300)) + [4096, 4095, 1000, 111 - 64 + 64]:
+        R = bytes(r.getrandbits(8) for _ in range(32))
+        A = bytes(r.getrandbits(8) for _ in range(32))
+        m = bytes(r.getrandbits(8) for _ in range(n))
+        hc.hc_hram(R, A, m, len(m), d)
+        assert d.raw == hashlib.sha512(R + A + m).digest(), n
+
+
+def test_kernel_algorithm_on_cpu_matches_libsodium_golden(golden, golden_meta):
+    hc = hostcheck_lib.load()
+    sigs, pks, msgs, off = golden_io.pack_batch(golden)
+    acc = ctypes.create_string_buffer(len(golden))
+    hc.hc_verify_batch(sigs, pks, msgs or b"\0", off.ctypes.data, len(golden), acc)
+    cats = golden_meta["categories"]
+    bad = [(i, cats[g[1]]) for i, g in enumerate(golden) if acc.raw[i] != g[0]]
+    assert bad == []
