@@ -1,0 +1,179 @@
+#!/usr/bin/env python3
+"""Benchmark: Ed25519 verifies/s on MI355X for Plenum's client-request
+authentication hot path (BASELINE.json metric), with the INT32-VALU roofline
+fraction and the libsodium CPU baseline timed on the same box.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--msg-len 256]
+
+A "step" = one pass of the verifier (prep + main kernels) over one batch of B
+synthetic signed requests resident in HBM (default B = 65,536 x 256-byte
+NYM-shaped messages, distinct signers: BASELINE.json configs[1]).  With N > 1
+(launched by torch.distributed.run) every rank verifies its own B-request shard
+of the request index space: weak scaling, no collective on the data path; the
+per-request accept bytes are checked after the timed region.
+
+The verify inputs are produced by the product's own GPU batch signer (row f-4),
+never by the oracle; only the cpu_baseline leg uses oracle/ (the libsodium
+harness oracle/sodium_batch.c, i.e. the reference's own CPU path).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+from indy_plenum_amd import edv, workload  # noqa: E402
+
+# Algorithmic INT32 work per verify:
+#   W(m) = 217,600 + 5,500 * ceil((m + 81) / 128)   (3,400 GF(p) mul/sq x 64 u32 mul-adds + SHA-512 blocks)
+# split by kernel: main = V8 loop + V9 encode = (2,737 + 267) x 64; prep = the rest.
+MAIN_OPS = (2737 + 267) * 64
+
+
+def w_total(m):
+    return 217600 + 5500 * -(-(m + 81) // 128)
+
+
+# INT32 VALU peak: 256 CUs x 64 lanes/clk (4 SIMDs at the 4-cycle VOP3 rate that
+# v_mad_i64_i32 / v_mad_u64_u32 issue at, tools/ubench_valu.hip) x 2.4 GHz.
+PEAK_INT32 = 256 * 64 * 2.4e9
+
+
+def cpu_baseline(batch, budget_s):
+    """libsodium 1.0.18 verify_detached over the same batch on the host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as orc  # the baseline leg is the only oracle/ user here
+    sb = orc.sodium_batch()
+    sigs, pks, msgs, off = batch.host_copy()
+    if sb is None:
+        return None
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(16, ncpu))  # the GPU box's CPU share for one GPU is 16 threads
+    acc = orc.sodium_verify_batch(sigs, pks, msgs, off, threads)  # warm + sanity
+    assert acc.all()
+    n = batch.n
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        orc.sodium_verify_batch(sigs, pks, msgs, off, threads)
+        done += n
+    dt = time.perf_counter() - t0
+    # single-thread reference point on a smaller slice
+    k = min(n, 16384)
+    o1 = off[:k + 1]
+    t1 = time.perf_counter()
+    orc.sodium_verify_batch(sigs[:64 * k], pks[:32 * k], msgs, o1, 1)
+    one = k / (time.perf_counter() - t1)
+    return {"value": done / dt, "unit": "verifies/s", "cores": threads, "kind": "reference",
+            "sample": "%d passes over the %d-request batch (%d B msgs): libsodium %s crypto_sign_ed25519_verify_detached "
+                      "(oracle/sodium_batch.c), %d threads, %.1f s; 1 thread: %.0f verifies/s"
+                      % (done // n, n, int(off[1] - off[0]), sb.sb_version().decode(), threads, dt, one)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=65536, help="requests per GPU per step")
+    ap.add_argument("--msg-len", type=int, default=256)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")  # RCCL over xGMI
+        dist = tdist
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    dev = local
+    n = args.batch
+    # this rank's shard of the request index space: [rank * n, (rank + 1) * n)
+    batch = workload.DeviceBatch(n, device=dev, start=rank * n, msg_len=args.msg_len)
+
+    for _ in range(args.warmup):
+        batch.verify()
+    ok = batch.accept()
+    assert ok.all(), "warm-up verify rejected %d valid signatures" % int((ok == 0).sum())
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        batch.verify()  # synchronous on the library stream of this device
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = max_over_ranks(t1 - t0)
+    ms_step = 1e3 * elapsed / args.steps
+    total = n * world * args.steps
+    value = total / elapsed
+
+    # per-kernel durations (HIP events on the kernels' own stream), same batch
+    iters = max(3, min(args.steps, 10))
+    prep_ms, main_ms = edv.profile_device(batch.d_sigs.ptr, batch.d_pks.ptr, batch.d_msgs.ptr, batch.d_off.ptr, n,
+                                          batch.d_accept.ptr, dev, iters)
+    ok = batch.accept()
+    all_ok = max_over_ranks(0.0 if ok.all() else 1.0) == 0.0
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    achieved = MAIN_OPS * n / (main_ms * 1e-3)
+    whole = w_total(args.msg_len) * n / ((prep_ms + main_ms) * 1e-3)
+    out = {
+        "metric": "Ed25519 verifies/sec (256B msgs) + % of INT32 VALU peak",
+        "value": value,
+        "unit": "verifies/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic: NYM-shaped signing bytes, distinct signers, keys+signatures made by the GPU batch signer",
+        "config": {"workload": "C2: %d Ed25519 verifies per GPU per step, fixed %d-byte serialized requests, distinct "
+                               "signers%s" % (n, args.msg_len, "" if world == 1 else "; C3-style shard by request index"),
+                   "batch_per_gpu": n, "msg_len": args.msg_len, "parallelism": "shard-by-request-index x%d" % world},
+        "roofline": {"bound": "valu_int32", "kernel": "edv_main_kernel",
+                     "achieved": achieved / 1e12, "peak": PEAK_INT32 / 1e12, "unit": "TOP/s",
+                     "frac": achieved / PEAK_INT32, "traffic": None,
+                     "ops_per_launch": MAIN_OPS * n, "kernel_ms": main_ms, "prep_kernel_ms": prep_ms,
+                     "whole_path_frac": whole / PEAK_INT32},
+        "all_accepted": bool(all_ok),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(batch, args.cpu_seconds)
+        out["cpu_baseline"] = cb
+        if cb:
+            out["gpu_over_cpu"] = value / cb["value"]
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

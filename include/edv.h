@@ -75,6 +75,31 @@ int edv_time_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_
                        const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept, int device,
                        int iters, float *ms_out);
 
+/*
+ * Measurement helper: average per-launch milliseconds of the two kernels of
+ * one batch (n <= chunk), each bracketed by HIP events on the kernel's stream:
+ * prep (checks, decompression, SHA-512, table) and main (scalar mult, encode).
+ */
+int edv_profile_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
+                          const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept, int device,
+                          int iters, float *ms_prep, float *ms_main);
+
+/* Signatures per prep/main kernel pair on `device` (0 = default 2^18; rounded
+ * down to a multiple of 256).  Tuning/testing knob: verdicts never depend on it. */
+int edv_set_chunk(int device, uint64_t chunk);
+
+/*
+ * Batch Ed25519 signing for synthetic load generation,
+ * device-resident: seeds n x 32 B -> pks n x 32 B and detached sigs n x 64 B
+ * over the given messages; RFC 8032 deterministic, byte-identical to libsodium
+ * crypto_sign_seed_keypair + crypto_sign_detached.  Counterpart of the
+ * reference's client-side signing (stp_core/crypto/nacl_wrappers.py:162-176
+ * SigningKey.sign, plenum/common/signer_did.py:122-129).  Async on `stream`
+ * (NULL = library stream, synchronised before returning).
+ */
+int edv_sign_batch_dev(const uint8_t *d_seeds, const uint8_t *d_msgs, const uint64_t *d_msg_off, uint64_t msg_base,
+                       uint64_t n, uint8_t *d_pks, uint8_t *d_sigs, int device, void *stream);
+
 /* Number of visible gfx950 devices (0 if none). */
 int edv_device_count(void);
 

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <mutex>
 #include <thread>
@@ -32,6 +33,19 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kAWords = kAEntries * 40;   // cached point = 4 x 10 limbs
+constexpr uint64_t kChunkDefault = uint64_t(1) << 18;  // signatures per prep/main launch pair
+
+// Per-chunk state handed from the prep kernel to the main kernel, SoA so every
+// wave-wide load/store touches 64 consecutive words:
+//   atab[w * cap + i]  word w (0..319) of signature i's 1..8 x (-A) table
+//   dig[w * cap + i]   w 0..7: packed radix-16 digits of h, 8..15: radix-256 digits of S
+//   alive[i]           1 if V2-V5 passed (the main kernel skips dead lanes' work)
+struct ChunkState {
+  int32_t* atab;
+  uint32_t* dig;
+  uint8_t* alive;
+  uint64_t cap;
+};
 
 struct VerifyArgs {
   const uint32_t* sigs;   // n x 16 words
@@ -39,15 +53,14 @@ struct VerifyArgs {
   const uint8_t* msgs;
   const uint64_t* off;    // n + 1
   uint64_t msg_base;
-  uint64_t n;
-  uint8_t* accept;
-  int32_t* atab;          // per-thread A tables: [kAWords][total threads]
+  uint64_t base;          // first signature of this chunk
+  uint64_t n;             // signatures in this chunk
+  uint8_t* accept;        // indexed by global signature index
+  ChunkState st;
   const int32_t* btab;    // kBEntries x kBStride
 };
 
 // ---------------------------------------------------------------- kernels
-// Per-thread A table in a global scratch buffer: word w of thread g at
-// slot[w * nthreads], so each load/store of a wave touches 64 consecutive words.
 struct GlobalATab {
   int32_t* slot;
   uint64_t stride;
@@ -84,31 +97,97 @@ struct LdsBTab {
   }
 };
 
-__global__ __launch_bounds__(kBlock) void edv_verify_kernel(VerifyArgs a) {
-  __shared__ __attribute__((aligned(16))) int32_t btab[kBEntries * kBStride];
-  for (int i = threadIdx.x; i < kBEntries * kBStride / 4; i += kBlock)
-    reinterpret_cast<int4*>(btab)[i] = reinterpret_cast<const int4*>(a.btab)[i];
-  __syncthreads();
-
-  const uint64_t nthreads = uint64_t(gridDim.x) * kBlock;
-  const uint64_t gtid = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-  GlobalATab at{a.atab + gtid, nthreads};
-  const LdsBTab bt{btab};
-
-  for (uint64_t i = gtid; i < a.n; i += nthreads) {
-    uint32_t R[8], S[8], A[8];
-    const uint4* sp = reinterpret_cast<const uint4*>(a.sigs + 16 * i);
-    const uint4* pp = reinterpret_cast<const uint4*>(a.pks + 8 * i);
+__device__ __forceinline__ void load_words(uint32_t* out, const uint32_t* p, int n4) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const uint4 r = sp[k], s = sp[2 + k], p = pp[k];
-      R[4 * k] = r.x; R[4 * k + 1] = r.y; R[4 * k + 2] = r.z; R[4 * k + 3] = r.w;
-      S[4 * k] = s.x; S[4 * k + 1] = s.y; S[4 * k + 2] = s.z; S[4 * k + 3] = s.w;
-      A[4 * k] = p.x; A[4 * k + 1] = p.y; A[4 * k + 2] = p.z; A[4 * k + 3] = p.w;
-    }
-    const uint64_t o0 = a.off[i] - a.msg_base, o1 = a.off[i + 1] - a.msg_base;
-    a.accept[i] = verify_one(R, S, A, a.msgs + o0, o1 - o0, at, bt) ? 1 : 0;
+  for (int k = 0; k < n4; k++) {
+    const uint4 v = q[k];
+    out[4 * k] = v.x; out[4 * k + 1] = v.y; out[4 * k + 2] = v.z; out[4 * k + 3] = v.w;
   }
+}
+
+// Phase 1: V2-V7, digit recoding, the per-signature A table.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 8))) void edv_prep_kernel(VerifyArgs a) {
+  const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;  // index within the chunk
+  if (j >= a.n) return;
+  const uint64_t i = a.base + j;
+  uint32_t R[8], S[8], A[8];
+  load_words(R, a.sigs + 16 * i, 2);
+  load_words(S, a.sigs + 16 * i + 8, 2);
+  load_words(A, a.pks + 8 * i, 2);
+  const uint64_t o0 = a.off[i] - a.msg_base, o1 = a.off[i + 1] - a.msg_base;
+  GlobalATab at{a.st.atab + j, a.st.cap};
+  uint32_t hd[8], sd[8];
+  const bool ok = prep_one(R, S, A, a.msgs + o0, o1 - o0, at, hd, sd);
+  a.st.alive[j] = ok ? 1 : 0;
+  if (ok) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      a.st.dig[uint64_t(k) * a.st.cap + j] = hd[k];
+      a.st.dig[uint64_t(8 + k) * a.st.cap + j] = sd[k];
+    }
+  } else {
+    a.accept[i] = 0;
+  }
+}
+
+// Phase 2: V8 double-scalar multiplication and V9 compare (~85% of the work).
+__global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
+  __shared__ __attribute__((aligned(16))) int32_t btab[kBEntries * kBStride];
+  for (int t = threadIdx.x; t < kBEntries * kBStride / 4; t += kBlock)
+    reinterpret_cast<int4*>(btab)[t] = reinterpret_cast<const int4*>(a.btab)[t];
+  __syncthreads();
+  const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= a.n || !a.st.alive[j]) return;
+  const uint64_t i = a.base + j;
+  uint32_t R[8], hd[8], sd[8];
+  load_words(R, a.sigs + 16 * i, 2);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    hd[k] = a.st.dig[uint64_t(k) * a.st.cap + j];
+    sd[k] = a.st.dig[uint64_t(8 + k) * a.st.cap + j];
+  }
+  const GlobalATab at{a.st.atab + j, a.st.cap};
+  const LdsBTab bt{btab};
+  a.accept[i] = main_one(R, hd, sd, at, bt) ? 1 : 0;
+}
+
+// Comb rows for the batch signer, in global memory (528 KB, L2-resident).
+struct GlobalComb {
+  const int32_t* w;
+  __device__ __forceinline__ ge_precomp entry(int i, int j) const {
+    const int4* p = reinterpret_cast<const int4*>(w + (i * kBEntries + j) * kBStride);
+    int32_t t[32];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int4 v = p[k];
+      t[4 * k] = v.x; t[4 * k + 1] = v.y; t[4 * k + 2] = v.z; t[4 * k + 3] = v.w;
+    }
+    return precomp_from_words(t);
+  }
+};
+
+// Batch signer (row f-4: synthetic load generation): seeds -> (pk, sig) over M.
+__global__ __launch_bounds__(kBlock) void edv_sign_kernel(const uint32_t* seeds, const uint8_t* msgs,
+                                                          const uint64_t* off, uint64_t msg_base, uint64_t n,
+                                                          uint32_t* pks, uint32_t* sigs, const int32_t* comb) {
+  const uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint32_t seed[8], pk[8], sig[16];
+  load_words(seed, seeds + 8 * i, 2);
+  const uint64_t o0 = off[i] - msg_base, o1 = off[i + 1] - msg_base;
+  sign_one(pk, sig, seed, msgs + o0, o1 - o0, GlobalComb{comb});
+  uint4* po = reinterpret_cast<uint4*>(pks + 8 * i);
+  uint4* so = reinterpret_cast<uint4*>(sigs + 16 * i);
+  po[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+  po[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+#pragma unroll
+  for (int k = 0; k < 4; k++) so[k] = make_uint4(sig[4 * k], sig[4 * k + 1], sig[4 * k + 2], sig[4 * k + 3]);
+}
+
+__global__ void edv_comb_kernel(int32_t* out) {
+  const int t = threadIdx.x + blockIdx.x * blockDim.x;
+  if (t < kCombRows * kBEntries) comb_entry(out + t * kBStride, t / kBEntries, t % kBEntries);
 }
 
 // j * B for j = 0..128 in affine precomp form, once per device
@@ -152,8 +231,9 @@ struct DevCtx {
   int dev = -1;
   hipStream_t stream = nullptr;
   int32_t* btab = nullptr;
-  int max_blocks = 0;   // grid cap: resident blocks on the whole device
-  DevBuf atab;          // per-thread A tables (grid cap x 256 x 1280 B)
+  int32_t* comb = nullptr;         // signer comb table, built on first edv_sign_* call
+  uint64_t chunk = kChunkDefault;  // EDV_CHUNK overrides (tests exercise chunk seams)
+  DevBuf atab, dig, alive;  // ChunkState storage for `chunk` signatures (~350 MB at 2^18)
   DevBuf sigs, pks, msgs, off, acc;
 };
 
@@ -179,11 +259,12 @@ int ctx_init(DevCtx& c, int dev) {
   HIPOK(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties");
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return set_err(EDV_E_NODEV, "device is not gfx950");
   HIPOK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking), "hipStreamCreate");
-  int per_cu = 0;
-  HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, edv_verify_kernel, kBlock, 0), "occupancy");
-  if (per_cu < 1) per_cu = 1;
-  c.max_blocks = per_cu * prop.multiProcessorCount;
-  if (c.atab.ensure(uint64_t(c.max_blocks) * kBlock * kAWords * 4)) return EDV_E_OOM;
+  if (const char* e = getenv("EDV_CHUNK")) {
+    const uint64_t v = strtoull(e, nullptr, 10);
+    if (v >= kBlock && v <= (uint64_t(1) << 24)) c.chunk = (v / kBlock) * kBlock;
+  }
+  if (c.atab.ensure(c.chunk * kAWords * 4) || c.dig.ensure(c.chunk * 16 * 4) || c.alive.ensure(c.chunk))
+    return EDV_E_OOM;
   HIPOK(hipMalloc(&c.btab, kBEntries * kBStride * 4), "hipMalloc btab");
   edv_btab_kernel<<<(kBEntries + 63) / 64, 64, 0, c.stream>>>(c.btab);
   HIPOK(hipGetLastError(), "btab launch");
@@ -200,24 +281,29 @@ DevCtx* get_ctx(int dev, int* err) {
   return g_ctx[dev];
 }
 
-// launch on ctx stream or the given stream; caller holds c.mu
+// launch on ctx stream or the given stream; caller holds c.mu.  The batch is
+// walked in chunks of kChunk signatures: prep kernel, then main kernel.
 int launch(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_off,
            uint64_t msg_base, uint64_t n, uint8_t* d_accept, hipStream_t s) {
-  if (n == 0) return 0;
-  uint64_t blocks = (n + kBlock - 1) / kBlock;
-  if (blocks > uint64_t(c.max_blocks)) blocks = c.max_blocks;
   VerifyArgs va;
   va.sigs = reinterpret_cast<const uint32_t*>(d_sigs);
   va.pks = reinterpret_cast<const uint32_t*>(d_pks);
   va.msgs = d_msgs;
   va.off = d_off;
   va.msg_base = msg_base;
-  va.n = n;
   va.accept = d_accept;
-  va.atab = static_cast<int32_t*>(c.atab.p);
+  va.st = ChunkState{static_cast<int32_t*>(c.atab.p), static_cast<uint32_t*>(c.dig.p),
+                     static_cast<uint8_t*>(c.alive.p), c.chunk};
   va.btab = c.btab;
-  edv_verify_kernel<<<dim3(unsigned(blocks)), dim3(kBlock), 0, s>>>(va);
-  HIPOK(hipGetLastError(), "verify launch");
+  for (uint64_t base = 0; base < n; base += c.chunk) {
+    va.base = base;
+    va.n = (n - base) < c.chunk ? (n - base) : c.chunk;
+    const unsigned blocks = unsigned((va.n + kBlock - 1) / kBlock);
+    edv_prep_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
+    HIPOK(hipGetLastError(), "prep launch");
+    edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
+    HIPOK(hipGetLastError(), "main launch");
+  }
   return 0;
 }
 
@@ -335,6 +421,100 @@ int edv_time_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   if (ms_out) *ms_out = ms;
+  return 0;
+}
+
+static int ensure_comb(DevCtx& c) {
+  if (c.comb) return 0;
+  HIPOK(hipMalloc(&c.comb, uint64_t(kCombRows) * kBEntries * kBStride * 4), "hipMalloc comb");
+  const int total = kCombRows * kBEntries;
+  edv_comb_kernel<<<(total + 63) / 64, 64, 0, c.stream>>>(c.comb);
+  HIPOK(hipGetLastError(), "comb launch");
+  HIPOK(hipStreamSynchronize(c.stream), "comb sync");
+  return 0;
+}
+
+int edv_sign_batch_dev(const uint8_t* d_seeds, const uint8_t* d_msgs, const uint64_t* d_msg_off, uint64_t msg_base,
+                       uint64_t n, uint8_t* d_pks, uint8_t* d_sigs, int device, void* stream) {
+  g_err.clear();
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((err = ctx_init(*c, device))) return err;
+  HIPOK(hipSetDevice(device), "hipSetDevice");
+  if ((err = ensure_comb(*c))) return err;
+  if (n == 0) return 0;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  const unsigned blocks = unsigned((n + kBlock - 1) / kBlock);
+  edv_sign_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(reinterpret_cast<const uint32_t*>(d_seeds), d_msgs,
+                                                        d_msg_off, msg_base, n, reinterpret_cast<uint32_t*>(d_pks),
+                                                        reinterpret_cast<uint32_t*>(d_sigs), c->comb);
+  HIPOK(hipGetLastError(), "sign launch");
+  if (!stream) HIPOK(hipStreamSynchronize(s), "stream sync");
+  return 0;
+}
+
+int edv_set_chunk(int device, uint64_t chunk) {
+  g_err.clear();
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((err = ctx_init(*c, device))) return err;
+  HIPOK(hipSetDevice(device), "hipSetDevice");
+  HIPOK(hipStreamSynchronize(c->stream), "stream sync");
+  if (chunk == 0) chunk = kChunkDefault;
+  if (chunk < kBlock || chunk > (uint64_t(1) << 24)) return set_err(EDV_E_ARG, "chunk out of range");
+  c->chunk = (chunk / kBlock) * kBlock;
+  if (c->atab.ensure(c->chunk * kAWords * 4) || c->dig.ensure(c->chunk * 16 * 4) || c->alive.ensure(c->chunk))
+    return EDV_E_OOM;
+  return 0;
+}
+
+int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
+                          const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, int device,
+                          int iters, float* ms_prep, float* ms_main) {
+  g_err.clear();
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((err = ctx_init(*c, device))) return err;
+  HIPOK(hipSetDevice(device), "hipSetDevice");
+  if (n == 0 || n > c->chunk) return set_err(EDV_E_ARG, "profile needs 0 < n <= chunk");
+  VerifyArgs va;
+  va.sigs = reinterpret_cast<const uint32_t*>(d_sigs);
+  va.pks = reinterpret_cast<const uint32_t*>(d_pks);
+  va.msgs = d_msgs;
+  va.off = d_msg_off;
+  va.msg_base = msg_base;
+  va.accept = d_accept;
+  va.st = ChunkState{static_cast<int32_t*>(c->atab.p), static_cast<uint32_t*>(c->dig.p),
+                     static_cast<uint8_t*>(c->alive.p), c->chunk};
+  va.btab = c->btab;
+  va.base = 0;
+  va.n = n;
+  const unsigned blocks = unsigned((n + kBlock - 1) / kBlock);
+  hipEvent_t ev[3];
+  for (auto& e : ev) HIPOK(hipEventCreate(&e), "event");
+  float tp = 0, tm = 0;
+  for (int it = 0; it < iters; it++) {
+    HIPOK(hipEventRecord(ev[0], c->stream), "record");
+    edv_prep_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(va);
+    HIPOK(hipEventRecord(ev[1], c->stream), "record");
+    edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(va);
+    HIPOK(hipEventRecord(ev[2], c->stream), "record");
+    HIPOK(hipEventSynchronize(ev[2]), "event sync");
+    float a = 0, b = 0;
+    HIPOK(hipEventElapsedTime(&a, ev[0], ev[1]), "elapsed");
+    HIPOK(hipEventElapsedTime(&b, ev[1], ev[2]), "elapsed");
+    tp += a;
+    tm += b;
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  if (ms_prep) *ms_prep = tp / iters;
+  if (ms_main) *ms_main = tm / iters;
   return 0;
 }
 

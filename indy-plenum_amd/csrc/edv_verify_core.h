@@ -42,24 +42,26 @@ EDV_HD uint64_t msg_word(const uint8_t* m, uint64_t mlen, uint64_t q) {
   return be64_from_le_words(uint32_t(v), uint32_t(v >> 32));
 }
 
-// SHA-512(R || A || M) -> 16 little-endian words of the 64-byte digest (V6)
-EDV_HD void hram(uint32_t out[16], const uint32_t R[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen) {
+// SHA-512(P || M) for a 32- or 64-byte prefix P given as little-endian words,
+// -> 16 little-endian words of the 64-byte digest.
+template <int PB>
+EDV_HD void sha512_pm(uint32_t out[16], const uint32_t* P, const uint8_t* m, uint64_t mlen) {
+  static_assert(PB == 32 || PB == 64, "prefix is 32 or 64 bytes");
   uint64_t H[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
                    0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
-  const uint64_t total = 64 + mlen;
+  constexpr int PW = PB / 8;  // prefix 64-bit SHA words
+  const uint64_t total = PB + mlen;
   const uint64_t nb = (total + 17 + 127) / 128;
   uint64_t W[16];
 #pragma unroll
-  for (int t = 0; t < 4; t++) W[t] = be64_from_le_words(R[2 * t], R[2 * t + 1]);
+  for (int t = 0; t < PW; t++) W[t] = be64_from_le_words(P[2 * t], P[2 * t + 1]);
 #pragma unroll
-  for (int t = 0; t < 4; t++) W[4 + t] = be64_from_le_words(A[2 * t], A[2 * t + 1]);
-#pragma unroll
-  for (int t = 8; t < 16; t++) W[t] = msg_word(m, mlen, uint64_t(8 * (t - 8)));
+  for (int t = PW; t < 16; t++) W[t] = msg_word(m, mlen, uint64_t(8 * (t - PW)));
   if (nb == 1) { W[14] = total >> 61; W[15] = total << 3; }
   sha512_compress(H, W);
 #pragma unroll 1
   for (uint64_t b = 1; b < nb; b++) {
-    const uint64_t q0 = 128 * b - 64;
+    const uint64_t q0 = 128 * b - PB;
 #pragma unroll
     for (int t = 0; t < 16; t++) W[t] = msg_word(m, mlen, q0 + 8 * t);
     if (b == nb - 1) { W[14] = total >> 61; W[15] = total << 3; }
@@ -70,6 +72,14 @@ EDV_HD void hram(uint32_t out[16], const uint32_t R[8], const uint32_t A[8], con
     out[2 * i] = bswap32(uint32_t(H[i] >> 32));
     out[2 * i + 1] = bswap32(uint32_t(H[i]));
   }
+}
+
+// SHA-512(R || A || M) (V6)
+EDV_HD void hram(uint32_t out[16], const uint32_t R[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen) {
+  uint32_t P[16];
+#pragma unroll
+  for (int k = 0; k < 8; k++) { P[k] = R[k]; P[8 + k] = A[k]; }
+  sha512_pm<64>(out, P, m, mlen);
 }
 
 // ------------------------------------------------------------ scalar recoding
@@ -144,41 +154,42 @@ EDV_HD void btab_entry(int32_t* o, int j) {
   o[31] = 0;
 }
 
-// The whole verdict for one signature.  ATab provides store(e, cached) /
-// load(e) for this lane's 1..8 x (-A) table; BTab provides entry(j) -> precomp.
-// Returns true iff libsodium's verify_detached would return 0.
-template <class ATab, class BTab>
-EDV_HD bool verify_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen,
-                       ATab& at, const BTab& bt) {
-  // V2-V4: strictness on bytes
+// Phase 1 of one signature (kernel edv_prep_kernel): strictness checks V2-V4,
+// decompression V5, h = SHA-512(R || A || M) mod L (V6, V7), digit recoding and
+// the 1..8 x (-A) table.  Returns false if the signature is already rejected
+// (then hd/sd/table are unspecified).  ATab provides store(e, cached).
+template <class ATab>
+EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen,
+                     ATab& at, uint32_t hd[8], uint32_t sd[8]) {
   bool ok = !((S[7] & 0xF0000000u) && !sc_is_canonical(S));
   ok = ok && !has_small_order(R);
   ok = ok && ge_is_canonical(A) && !has_small_order(A);
   if (!ok) return false;
-  // V5
   ge_p3 nA;
   if (!ge_frombytes_negate(nA, A)) return false;
-  // V6, V7
   uint32_t dig[16], h[8];
   hram(dig, R, A, m, mlen);
   sc_reduce(h, dig);
-  uint32_t hd[8], sd[8];
   recode4(hd, h);
   recode8(sd, S);
-  // table 1..8 x (-A)
-  {
-    const ge_cached c1 = ge_p3_to_cached(nA);
-    at.store(0, c1);
-    ge_p3 cur = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(nA)));
-    at.store(1, ge_p3_to_cached(cur));
+  const ge_cached c1 = ge_p3_to_cached(nA);
+  at.store(0, c1);
+  ge_p3 cur = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(nA)));
+  at.store(1, ge_p3_to_cached(cur));
 #pragma unroll 1
-    for (int e = 2; e < kAEntries; e++) {
-      cur = ge_p1p1_to_p3(ge_add(cur, c1));
-      at.store(e, ge_p3_to_cached(cur));
-    }
+  for (int e = 2; e < kAEntries; e++) {
+    cur = ge_p1p1_to_p3(ge_add(cur, c1));
+    at.store(e, ge_p3_to_cached(cur));
   }
-  // V8: joint fixed-window double-scalar multiplication, top digit first.  Every
-  // lane adds at the same positions, so a wave never diverges here.
+  return true;
+}
+
+// Phase 2 (kernel edv_main_kernel): V8 R' = [h](-A) + [S]B by a joint
+// fixed-window walk, top digit first -- every lane adds at the same positions,
+// so a wave never diverges -- then V9 encode(R') == R.  ATab provides load(e);
+// BTab provides entry(j) -> precomp.
+template <class ATab, class BTab>
+EDV_HD bool main_one(const uint32_t R[8], uint32_t hd[8], uint32_t sd[8], const ATab& at, const BTab& bt) {
   ge_p2 acc = ge_p2_identity();
 #pragma unroll 1
   for (int w = 63; w >= 0; --w) {
@@ -208,13 +219,114 @@ EDV_HD bool verify_one(const uint32_t R[8], const uint32_t S[8], const uint32_t 
     }
     acc = ge_p1p1_to_p2(t);
   }
-  // V9
   uint32_t enc[8];
   ge_p2_tobytes(enc, acc);
   bool match = true;
 #pragma unroll
   for (int k = 0; k < 8; k++) match = match && (enc[k] == R[k]);
   return match;
+}
+
+// The whole verdict for one signature: true iff libsodium's verify_detached
+// would return 0.
+template <class ATab, class BTab>
+EDV_HD bool verify_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen,
+                       ATab& at, const BTab& bt) {
+  uint32_t hd[8], sd[8];
+  if (!prep_one(R, S, A, m, mlen, at, hd, sd)) return false;
+  return main_one(R, hd, sd, at, bt);
+}
+
+// ------------------------------------------------ batch signing (row f-4)
+// Fixed-base comb for [k]B without doublings: entry (i, j) = j * 256^i * B,
+// i < 32, j <= 128, affine precomp form; [k]B = sum_i T[i][d_i] over the signed
+// radix-256 digits of k < L.
+constexpr int kCombRows = 32;
+EDV_HD void comb_entry(int32_t* o, int i, int j) {
+  const uint32_t Bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                          0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+  ge_p3 nB;
+  ge_frombytes_negate(nB, Bw);
+  ge_p3 base{fe_neg(nB.X), nB.Y, nB.Z, fe_neg(nB.T)};
+  for (int k = 0; k < 8 * i; k++) base = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(base)));
+  const ge_cached bc = ge_p3_to_cached(base);
+  ge_p3 acc = ge_p3_identity();
+  for (int bit = 7; bit >= 0; bit--) {
+    acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
+    if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add(acc, bc));
+  }
+  const fe zi = fe_invert(acc.Z);
+  const fe x = fe_mul(acc.X, zi), y = fe_mul(acc.Y, zi);
+  const fe ypx = fe_carry32(fe_add(y, x)), ymx = fe_carry32(fe_sub(y, x));
+  const fe xy2d = fe_mul(fe_mul(x, y), fe_d2());
+  for (int l = 0; l < 10; l++) { o[l] = ypx.v[l]; o[10 + l] = ymx.v[l]; o[20 + l] = xy2d.v[l]; }
+  o[30] = 0;
+  o[31] = 0;
+}
+// [k]B for k < L (8 words); CombTab provides entry(i, j) -> precomp
+template <class CombTab>
+EDV_HD ge_p3 scalarmult_base(const uint32_t k[8], const CombTab& ct) {
+  uint32_t d[8];
+  recode8(d, k);
+  ge_p3 acc = ge_p3_identity();
+#pragma unroll 1
+  for (int i = 0; i < kCombRows; i++) {
+    const int di = int(int8_t(uint8_t(d[i >> 2] >> (8 * (i & 3)))));
+    const int ui = di < 0 ? -di : di;
+    acc = ge_p1p1_to_p3(ge_madd(acc, ge_precomp_cneg(ct.entry(i, ui), di < 0)));
+  }
+  return acc;
+}
+EDV_HD void ge_p3_tobytes(uint32_t w[8], const ge_p3& p) { ge_p2_tobytes(w, ge_p3_to_p2(p)); }
+
+// (a * b + c) mod L for 8-word little-endian scalars
+EDV_HD void sc_muladd(uint32_t out[8], const uint32_t a[8], const uint32_t b[8], const uint32_t c[8]) {
+  uint32_t t[16];
+  uint64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    // column k of a*b (+ c_k): accumulate 32x32 products into a 96-bit column sum
+    uint64_t lo = carry + (k < 8 ? c[k] : 0), hi = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (j < 0 || j > 7) continue;
+      const uint64_t p = uint64_t(a[i]) * b[j];
+      const uint64_t s = lo + p;
+      hi += (s < lo);
+      lo = s;
+    }
+    t[k] = uint32_t(lo);
+    carry = (lo >> 32) | (hi << 32);
+  }
+  sc_reduce(out, t);
+}
+
+// RFC 8032 / libsodium crypto_sign_seed_keypair + crypto_sign_detached for one
+// (seed, M): deterministic, so results are comparable byte for byte.
+template <class CombTab>
+EDV_HD void sign_one(uint32_t pk[8], uint32_t sig[16], const uint32_t seed[8], const uint8_t* m, uint64_t mlen,
+                     const CombTab& ct) {
+  uint32_t az[16];
+  sha512_pm<32>(az, seed, m, 0);
+  az[0] &= ~7u;
+  az[7] = (az[7] & 0x7fffffffu) | 0x40000000u;
+  uint32_t a64[16], a[8];
+#pragma unroll
+  for (int k = 0; k < 16; k++) a64[k] = k < 8 ? az[k] : 0;
+  sc_reduce(a, a64);  // [a]B = [a mod L]B; keeps the radix-256 digits in range
+  ge_p3_tobytes(pk, scalarmult_base(a, ct));
+  uint32_t nonce[16], r[8];
+  sha512_pm<32>(nonce, az + 8, m, mlen);
+  sc_reduce(r, nonce);
+  ge_p3_tobytes(sig, scalarmult_base(r, ct));
+  uint32_t hr[16], h[8];
+  hram(hr, sig, pk, m, mlen);
+  sc_reduce(h, hr);
+  uint32_t aclamped[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) aclamped[k] = az[k];
+  sc_muladd(sig + 8, h, aclamped, r);
 }
 
 }  // namespace edv

@@ -63,6 +63,13 @@ def lib():
         h.edv_time_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_float)]
         h.edv_time_batch_dev.restype = ctypes.c_int
+        h.edv_sign_batch_dev.argtypes = [vp, vp, vp, u64, u64, vp, vp, ctypes.c_int, vp]
+        h.edv_sign_batch_dev.restype = ctypes.c_int
+        h.edv_profile_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+        h.edv_profile_batch_dev.restype = ctypes.c_int
+        h.edv_set_chunk.argtypes = [ctypes.c_int, u64]
+        h.edv_set_chunk.restype = ctypes.c_int
         h.edv_device_count.argtypes = []
         h.edv_device_count.restype = ctypes.c_int
         h.edv_dev_alloc.argtypes = [ctypes.c_int, u64, ctypes.POINTER(ctypes.c_void_p)]
@@ -81,6 +88,11 @@ def version() -> str:
 
 def device_count() -> int:
     return lib().edv_device_count()
+
+
+def set_chunk(device: int, chunk: int):
+    """Signatures per prep/main kernel pair (0 = default).  Never changes verdicts."""
+    _check(lib().edv_set_chunk(device, chunk))
 
 
 def _check(rc):
@@ -198,9 +210,38 @@ def verify_device(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, msg_base=
     _check(lib().edv_verify_batch_dev(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, stream))
 
 
+def sign_device(d_seeds, d_msgs, d_off, n, d_pks, d_sigs, device=0, msg_base=0, stream=None):
+    """Device-resident batch signing (row f-4): seeds -> pks, detached sigs."""
+    _check(lib().edv_sign_batch_dev(d_seeds, d_msgs, d_off, msg_base, n, d_pks, d_sigs, device, stream))
+
+
+def sign_arrays(seeds, msgs, offsets, device=0):
+    """Host-array convenience over sign_device -> (pks n*32, sigs n*64) uint8 arrays."""
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(off) - 1
+    seeds = np.ascontiguousarray(np.frombuffer(bytes(seeds), np.uint8) if not isinstance(seeds, np.ndarray) else seeds)
+    msgs = np.frombuffer(bytes(msgs) + b"\0" * 16, np.uint8) if not isinstance(msgs, np.ndarray) else msgs
+    if n <= 0:
+        return np.zeros(0, np.uint8), np.zeros(0, np.uint8)
+    bufs = [DeviceBuffer(max(a.nbytes, 1) + 64, device) for a in (seeds, msgs, off)]
+    for b, a in zip(bufs, (seeds, msgs, off)):
+        b.upload(a)
+    dp, ds = DeviceBuffer(32 * n, device), DeviceBuffer(64 * n, device)
+    sign_device(bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, n, dp.ptr, ds.ptr, device)
+    return dp.download(32 * n), ds.download(64 * n)
+
+
 def time_device(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, iters=1, msg_base=0) -> float:
     """Milliseconds for `iters` back-to-back kernel launches (HIP events on the kernel's stream)."""
     ms = ctypes.c_float(0)
     _check(lib().edv_time_batch_dev(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, iters,
                                     ctypes.byref(ms)))
     return float(ms.value)
+
+
+def profile_device(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, iters=1, msg_base=0):
+    """(prep_ms, main_ms): average per-launch kernel times from HIP events on the kernels' stream."""
+    a, b = ctypes.c_float(0), ctypes.c_float(0)
+    _check(lib().edv_profile_batch_dev(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, iters,
+                                       ctypes.byref(a), ctypes.byref(b)))
+    return float(a.value), float(b.value)

@@ -44,6 +44,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
+#include <stdio.h>
 
 typedef unsigned __int128 u128;
 typedef struct { uint64_t v[5]; } fe;
@@ -593,6 +594,161 @@ int oref_verify_batch(const uint8_t *sigs, const uint8_t *pks, const uint8_t *ms
   for (int t = 0; t < threads; t++) {
     jobs[t] = (vjob){sigs, pks, msgs, off, accept, n * t / threads, n * (t + 1) / threads};
     if (pthread_create(&th[t], 0, vworker, &jobs[t])) return -1;
+  }
+  for (int t = 0; t < threads; t++) pthread_join(th[t], 0);
+  return 0;
+}
+
+/* ---------------------------------------------- deterministic corpus generator
+ * Test infrastructure: reproduces the same signed-request corpus from a 64-bit
+ * seed on any machine, so the GPU box can regenerate the >= 10M-case parity
+ * corpus whose libsodium verdict bitmask was computed in the build container
+ * (tests/golden/make_corpus_bitmask.py).  Item i depends only on (seed, i).
+ *
+ * mode 0: 256-byte NYM-shaped signing bytes (configs C2/C3)
+ * mode 1: lengths uniform in [200, 4096] (config C4)
+ * invalid_permille: share of items mutated into one of the section 8c
+ * categories (flipped M/R/S bit, S + L, wrong key, small-order A or R,
+ * mixed-order A with an honest signer, non-canonical A, off-curve A, garbage).
+ */
+static uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+uint64_t oref_corpus_len(uint64_t seed, uint64_t i, int mode) {
+  if (mode == 0) return 256;
+  return 200 + splitmix64(seed * 0x100000001B3ULL ^ i ^ 0xC4C4C4C4ULL) % 3897;
+}
+static const uint8_t T8_ENC[32] = {0x26, 0xe8, 0x95, 0x8f, 0xc2, 0xb2, 0x27, 0xb0, 0x45, 0xc3, 0xf4,
+                                   0x89, 0xf2, 0xef, 0x98, 0xf0, 0xd5, 0xdf, 0xac, 0x05, 0xd3, 0xc6,
+                                   0x33, 0x39, 0xb1, 0x38, 0x02, 0x88, 0x6d, 0x53, 0xfc, 0x05};
+static ge TORSION[8];
+static pthread_once_t g_tor_once = PTHREAD_ONCE_INIT;
+static void tor_init(void) {
+  oref_init();
+  ge t;
+  ge_frombytes_negate(&t, T8_ENC);
+  fe_neg(&t.X, &t.X);
+  fe_neg(&t.T, &t.T);
+  ge_identity(&TORSION[0]);
+  for (int k = 1; k < 8; k++) ge_add(&TORSION[k], &TORSION[k - 1], &t);
+}
+static void hexs(char *o, const uint8_t *b, int n) {
+  static const char *hx = "0123456789abcdef";
+  for (int i = 0; i < n; i++) { o[2 * i] = hx[b[i] >> 4]; o[2 * i + 1] = hx[b[i] & 15]; }
+}
+/* one item into sig/pk/msg (msg has oref_corpus_len bytes) */
+static void corpus_item(uint64_t seed, uint64_t i, int mode, int invalid_permille, uint8_t sig[64], uint8_t pk[32],
+                        uint8_t *msg) {
+  uint8_t in[24], ks[64], sk[64], aux[64];
+  memcpy(in, "edvcorp1", 8);
+  for (int k = 0; k < 8; k++) { in[8 + k] = (uint8_t)(seed >> (8 * k)); in[16 + k] = (uint8_t)(i >> (8 * k)); }
+  sha512_3(ks, in, 24, 0, 0, 0, 0);
+  sha512_3(aux, ks, 64, in, 24, 0, 0);
+  oref_seed_keypair(pk, sk, ks);
+  const uint64_t mlen = oref_corpus_len(seed, i, mode);
+  /* NYM-shaped bytes: identifier|operation(dest,type,verkey)|protocolVersion|reqId|zpad */
+  char buf[256];
+  char idh[33], dh[33], vh[33];
+  hexs(idh, pk, 16); idh[32] = 0;
+  hexs(dh, aux, 16); dh[32] = 0;
+  hexs(vh, pk + 16, 16); vh[32] = 0;
+  int hl = snprintf(buf, sizeof buf,
+                    "identifier:%s|operation:dest:%s|type:1|verkey:~%s|protocolVersion:2|reqId:%llu|zpad:", idh, dh,
+                    vh, (unsigned long long)(1539648000000000ULL + i));
+  uint64_t rs = splitmix64(seed ^ (i * 0x9E3779B97F4A7C15ULL));
+  for (uint64_t k = 0; k < mlen; k++) {
+    if ((int64_t)k < hl) msg[k] = (uint8_t)buf[k];
+    else { rs = splitmix64(rs); msg[k] = (uint8_t)('a' + rs % 26); }
+  }
+  oref_sign_detached(sig, msg, mlen, sk);
+  const unsigned pick = ((unsigned)aux[32] | (unsigned)aux[33] << 8) % 1000;
+  if ((int)pick >= invalid_permille) return;
+  const int cat = aux[34] % 11;
+  const int tk = 1 + aux[35] % 7;
+  switch (cat) {
+    case 0: msg[aux[36] % mlen] ^= (uint8_t)(1 << (aux[37] & 7)); break;  /* flip M */
+    case 1: sig[aux[36] % 32] ^= (uint8_t)(1 << (aux[37] & 7)); break;    /* flip R */
+    case 2: sig[32 + aux[36] % 31] ^= (uint8_t)(1 << (aux[37] & 7)); break; /* flip S (not the top byte) */
+    case 3: { /* S + L */
+      unsigned c = 0;
+      for (int k = 0; k < 32; k++) { c += sig[32 + k] + L_BYTES[k]; sig[32 + k] = (uint8_t)c; c >>= 8; }
+      break;
+    }
+    case 4: pk[aux[36] % 32] ^= (uint8_t)(1 << (aux[37] & 7)); break;      /* wrong / mangled key */
+    case 5: { /* small-order A */
+      pthread_once(&g_tor_once, tor_init);
+      ge_tobytes(pk, &TORSION[aux[36] & 7]);
+      if (aux[37] & 1) pk[31] ^= 0x80;
+      break;
+    }
+    case 6: { /* small-order R */
+      pthread_once(&g_tor_once, tor_init);
+      ge_tobytes(sig, &TORSION[aux[36] & 7]);
+      break;
+    }
+    case 7: { /* mixed-order A = A0 + T, honest signer: accept iff [h]T = 0 */
+      pthread_once(&g_tor_once, tor_init);
+      uint8_t az[64], r[32], h[32], nonce[64], hram_[64];
+      sha512_3(az, ks, 32, 0, 0, 0, 0);
+      az[0] &= 248; az[31] &= 127; az[31] |= 64;
+      ge A0, A;
+      ge_scalarmult_base(&A0, az);
+      ge_add(&A, &A0, &TORSION[tk]);
+      ge_tobytes(pk, &A);
+      sha512_3(nonce, aux, 32, msg, mlen, 0, 0);
+      sc_mod(r, nonce, 64);
+      ge R;
+      ge_scalarmult_base(&R, r);
+      ge_tobytes(sig, &R);
+      sha512_3(hram_, sig, 32, pk, 32, msg, mlen);
+      sc_mod(h, hram_, 64);
+      sc_muladd(sig + 32, h, az, r);
+      break;
+    }
+    case 8: { /* non-canonical A: y + p for small y */
+      memset(pk, 0xff, 32);
+      pk[0] = (uint8_t)(0xed + aux[36] % 19);
+      pk[31] = (uint8_t)(0x7f | (aux[37] & 0x80));
+      break;
+    }
+    case 9: { /* off-curve A: y = 2..11 */
+      memset(pk, 0, 32);
+      pk[0] = (uint8_t)(2 + aux[36] % 10);
+      break;
+    }
+    default: memcpy(sig, aux, 64); break; /* garbage signature */
+  }
+}
+typedef struct {
+  uint64_t seed, start, lo, hi;
+  int mode, inv;
+  uint8_t *sigs, *pks, *msgs;
+  const uint64_t *off;
+} cjob;
+static void *cworker(void *arg) {
+  cjob *j = (cjob *)arg;
+  for (uint64_t k = j->lo; k < j->hi; k++)
+    corpus_item(j->seed, j->start + k, j->mode, j->inv, j->sigs + 64 * k, j->pks + 32 * k, j->msgs + j->off[k]);
+  return 0;
+}
+/* Items [start, start + count) into caller buffers; off[count+1] must hold the
+ * cumulative oref_corpus_len values (relative to msgs). */
+int oref_corpus_gen(uint64_t seed, uint64_t start, uint64_t count, int mode, int invalid_permille, uint8_t *sigs,
+                    uint8_t *pks, uint8_t *msgs, const uint64_t *off, int threads) {
+  oref_init();
+  pthread_once(&g_tb_once, tb_init);
+  pthread_once(&g_tor_once, tor_init);
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  cjob jobs[256];
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (cjob){seed, start, count * t / threads, count * (t + 1) / threads, mode, invalid_permille,
+                     sigs, pks, msgs, off};
+    if (pthread_create(&th[t], 0, cworker, &jobs[t])) return -1;
   }
   for (int t = 0; t < threads; t++) pthread_join(th[t], 0);
   return 0;

@@ -88,3 +88,74 @@ def verify_batch(sigs: bytes, pks: bytes, msgs: bytes, offs, n: int, threads: in
     rc = load().oref_verify_batch(sigs, pks, msgs if msgs else b"\0", off.ctypes.data, n, acc, threads)
     assert rc == 0
     return acc.raw[:n]
+
+
+def corpus_lengths(seed: int, start: int, count: int, mode: int):
+    import numpy as np
+    lib = load()
+    lib.oref_corpus_len.restype = ctypes.c_uint64
+    lib.oref_corpus_len.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]
+    if mode == 0:
+        return np.full(count, 256, dtype=np.uint64)
+    # same splitmix64 as the C generator, vectorised
+    x = (np.uint64(seed) * np.uint64(0x100000001B3)) ^ (np.arange(start, start + count, dtype=np.uint64)) ^ np.uint64(0xC4C4C4C4)
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+    return np.uint64(200) + x % np.uint64(3897)
+
+
+def corpus(seed: int, start: int, count: int, mode: int = 0, invalid_permille: int = 50, threads: int = None):
+    """Deterministic signed-request corpus (items [start, start+count)):
+    -> (sigs, pks, msgs, off) numpy uint8/uint64 arrays in the C-ABI layout."""
+    import numpy as np
+    lib = load()
+    threads = threads or min(16, os.cpu_count() or 1)
+    lens = corpus_lengths(seed, start, count, mode)
+    off = np.zeros(count + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    sigs = np.zeros(64 * count, dtype=np.uint8)
+    pks = np.zeros(32 * count, dtype=np.uint8)
+    msgs = np.zeros(int(off[-1]) + 64, dtype=np.uint8)
+    lib.oref_corpus_gen.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    rc = lib.oref_corpus_gen(seed, start, count, mode, invalid_permille, sigs.ctypes.data, pks.ctypes.data,
+                             msgs.ctypes.data, off.ctypes.data, threads)
+    assert rc == 0
+    return sigs, pks, msgs, off
+
+
+SODIUM_SO = os.path.join(ORACLE_DIR, "libsodium_batch.so")
+_sb = None
+
+
+def sodium_batch():
+    """libsodium 1.0.18 batch harness (oracle/sodium_batch.c) or None if the
+    image's libsodium is absent."""
+    global _sb
+    if _sb is None:
+        if not os.path.exists(SODIUM_SO):
+            subprocess.call(["make", "-s", "-C", ORACLE_DIR, "libsodium_batch.so"])
+        if not os.path.exists(SODIUM_SO):
+            return None
+        try:
+            lib = ctypes.CDLL(SODIUM_SO)
+        except OSError:
+            return None
+        lib.sb_version.restype = ctypes.c_char_p
+        lib.sb_verify_batch.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
+        _sb = lib
+    return _sb
+
+
+def sodium_verify_batch(sigs, pks, msgs, off, threads: int = 1):
+    import numpy as np
+    lib = sodium_batch()
+    n = len(off) - 1
+    acc = np.zeros(n, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    assert lib.sb_verify_batch(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, off.ctypes.data, n,
+                               acc.ctypes.data, threads) == 0
+    return acc

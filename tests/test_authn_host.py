@@ -1,0 +1,310 @@
+"""Host logic of the authenticator mirror (client_authn.py, req_authenticator.py,
+verifier.py, nacl_wrappers.py) on CPU.  The GPU call edv.open_batch is replaced
+by the oracle here -- this suite checks the Python semantics (ordering,
+exceptions, thresholds, batching/replay), not the kernels; the same cases run
+on the GPU in tests/test_gpu_authn.py.
+
+Mirrors plenum/test/client/test_client_authn.py:39-74,
+plenum/test/client/test_core_authn.py:41-151, plenum/test/common/test_verifier.py,
+plenum/test/test_req_authenticator.py:16-80.
+"""
+import random
+
+import pytest
+
+import kats
+import oracle_lib as orc
+from indy_plenum_amd import base58, edv
+from indy_plenum_amd.client_authn import CoreAuthNr, SimpleAuthNr
+from indy_plenum_amd.exceptions import (CouldNotAuthenticate, EmptySignature, InsufficientCorrectSignatures,
+                                        InsufficientSignatures, InvalidKey, InvalidSignatureFormat,
+                                        MissingSignature, NoAuthenticatorFound, UnknownIdentifier)
+from indy_plenum_amd.req_authenticator import ReqAuthenticator
+from indy_plenum_amd.signing_serializer import serialize_msg_for_signing
+from indy_plenum_amd.verifier import DidVerifier
+
+IDR = '5G72199XZB7wREviUbQma7'
+MSG_STR = "42 (forty-two) is the natural number that succeeds 41 and precedes 43."
+
+
+def oracle_open_batch(items, device_mask=0):
+    """crypto_sign_open(sig + msg, pk) on the oracle, same contract as edv.open_batch."""
+    return [orc.sign_open(bytes(s) + bytes(m), bytes(p)) for s, m, p in items]
+
+
+@pytest.fixture(autouse=True)
+def cpu_checker(monkeypatch):
+    calls = []
+
+    def fake(items, device_mask=0):
+        items = list(items)
+        calls.append(len(items))
+        return oracle_open_batch(items)
+    monkeypatch.setattr(edv, "open_batch", fake)
+    return calls
+
+
+class Signer:
+    """SimpleSigner equivalent (plenum/common/signer_simple.py:23-70) on the oracle signer."""
+
+    def __init__(self, identifier=None, seed=None):
+        self.seed = seed or bytes(random.Random(id(self)).getrandbits(8) for _ in range(32))
+        self.pk, self.sk = orc.keypair(self.seed)
+        self.verkey = base58.b58encode(self.pk).decode()
+        self.identifier = identifier or self.verkey
+
+    def sign(self, msg):
+        return base58.b58encode(orc.sign(serialize_msg_for_signing(msg), self.sk)).decode()
+
+
+@pytest.fixture(scope="module")
+def signer():
+    return Signer(IDR, seed=b"A" * 32)
+
+
+@pytest.fixture()
+def sa(signer):
+    sa = CoreAuthNr()
+    sa.addIdr(signer.identifier, signer.verkey)
+    return sa
+
+
+@pytest.fixture(scope="module")
+def msg():
+    return {'myMsg': MSG_STR, 'identifier': IDR}
+
+
+def test_simple_authnr_verkey_none_raises():
+    class Dummy(SimpleAuthNr):
+        def getVerkey(self, _):
+            return None
+    s = Signer(seed=b"B" * 32)
+    m = dict(myMsg=MSG_STR)
+    d = Dummy()
+    d.addIdr(s.identifier, s.verkey)
+    with pytest.raises(CouldNotAuthenticate):
+        d.authenticate(m, s.identifier, s.sign(m))
+
+
+def test_core_missing_signature():
+    class Dummy(CoreAuthNr):
+        def getVerkey(self, _):
+            return None
+    with pytest.raises(MissingSignature):
+        Dummy().authenticate(dict(myMsg=MSG_STR), IDR)
+
+
+def test_client_authentication(sa, signer, msg):
+    assert sa.authenticate(msg, IDR, signer.sign(msg)) == [IDR]
+
+
+def test_message_modified(sa, signer, msg):
+    sig = signer.sign(msg)
+    msg2 = dict(msg)
+    msg2['myMsg'] = msg2['myMsg'][:-1] + '!'
+    with pytest.raises(InsufficientCorrectSignatures):
+        sa.authenticate(msg2, IDR, sig)
+
+
+def test_unknown_identifier(signer, msg):
+    with pytest.raises(UnknownIdentifier):
+        CoreAuthNr().authenticate(msg, IDR, signer.sign(msg))
+
+
+def test_invalid_signature_format(sa, msg):
+    with pytest.raises(InvalidSignatureFormat):
+        sa.authenticate(msg, IDR, "0OIl")
+
+
+def test_empty_signature_field():
+    sa = CoreAuthNr()
+    with pytest.raises(MissingSignature):
+        sa.authenticate({'identifier': IDR, 'signature': None, 'reqId': 1})
+    # an empty signature with no 'signatures' falls through to req['signatures'] (KeyError),
+    # as in the reference (client_authn.py:228-244)
+    with pytest.raises(KeyError):
+        sa.authenticate({'identifier': IDR, 'signature': '', 'reqId': 1})
+    assert EmptySignature.code == 121
+
+
+@pytest.fixture(scope="module")
+def signers():
+    return [Signer(seed=bytes([k]) * 32) for k in range(2, 5)]
+
+
+def test_verify_multi_sig_correct_and_threshold(signer, signers, msg):
+    sa = CoreAuthNr()
+    for c in [signer] + signers:
+        sa.addIdr(c.identifier, c.verkey)
+    correct = {c.identifier: c.sign(msg) for c in [signer] + signers}
+    idrs = list(correct.keys())
+    assert sa.authenticate_multi(msg, correct) == idrs
+    for i in range(1, 5):
+        got = sa.authenticate_multi(msg, correct, i)
+        assert got == idrs[:i]  # early break: the FIRST i correct ones, in dict order
+    two = {c.identifier: c.sign(msg) for c in [signer, signers[0]]}
+    two.update({c.identifier: c.sign({**msg, 'random_key': 11}) for c in signers[1:]})
+    assert sa.authenticate_multi(msg, two, 2) == list(two)[:2]
+    for th in (3, 4, None):
+        with pytest.raises(InsufficientCorrectSignatures):
+            sa.authenticate_multi(msg, two, th)
+    with pytest.raises(InsufficientSignatures):
+        sa.authenticate_multi(msg, {c.identifier: c.sign(msg) for c in [signer, signers[0]]}, 3)
+    with pytest.raises(InsufficientCorrectSignatures):
+        sa.authenticate_multi(msg, {})  # threshold 0, loop never breaks
+
+
+def test_exception_precedence_and_early_break(signer, signers, msg):
+    """A bad signature format AFTER the threshold is met is never reached;
+    before it, it is raised."""
+    sa = CoreAuthNr()
+    for c in [signer] + signers:
+        sa.addIdr(c.identifier, c.verkey)
+    good = [(c.identifier, c.sign(msg)) for c in [signer] + signers]
+    sigs = dict(good[:2] + [(signers[1].identifier, "0bad")])
+    assert sa.authenticate_multi(msg, sigs, 2) == [good[0][0], good[1][0]]
+    with pytest.raises(InvalidSignatureFormat):
+        sa.authenticate_multi(msg, sigs, 3)
+    sigs = dict([(signers[1].identifier, "0bad")] + good[:2])
+    with pytest.raises(InvalidSignatureFormat):
+        sa.authenticate_multi(msg, sigs, 1)
+
+
+def test_txn_types(sa):
+    assert sa.is_query("3") and not sa.is_write("3")
+    assert sa.is_write("0") and not sa.is_query("0")
+    assert sa.is_write("1") and not sa.is_query("1")
+    assert not sa.is_action("1")
+
+
+def test_did_verifier_fixtures():
+    v = DidVerifier(kats.SAMPLE_ABBR_VERKEY, identifier=kats.SAMPLE_IDENTIFIER)
+    assert v.verkey == kats.EXPECTED_VERKEY
+    for vk in (None, ''):
+        with pytest.raises(ValueError, match="'verkey' should be a non-empty string"):
+            DidVerifier(vk, identifier=kats.SAMPLE_IDENTIFIER)
+    with pytest.raises(InvalidKey, match='verkey {}'.format(kats.ODD_LENGTH_VERKEY)):
+        DidVerifier(kats.ODD_LENGTH_VERKEY)
+
+
+def test_kat1_cryptonym_request():
+    sa = CoreAuthNr()
+    sa.addIdr(kats.KAT1_IDR, '')  # cryptonym: the identifier is its own verkey
+    assert sa.authenticate(kats.kat1_request()) == [kats.KAT1_IDR]
+    for pv in (1, 2):
+        with pytest.raises(InsufficientCorrectSignatures):
+            sa.authenticate(kats.kat1_request(pv))
+
+
+def test_kat2_nym_request_abbreviated_verkey():
+    sa = CoreAuthNr()
+    sa.addIdr(kats.KAT2_IDR, kats.KAT2_ABBR_VERKEY)
+    assert sa.authenticate(kats.kat2_request(1)) == [kats.KAT2_IDR]
+    for pv in (None, 2):
+        with pytest.raises(InsufficientCorrectSignatures):
+            sa.authenticate(kats.kat2_request(pv))
+
+
+class DictState:
+    """Minimal state with the reference's get(key, isCommitted) contract."""
+
+    def __init__(self):
+        self.kv = {}
+
+    def get(self, key, isCommitted=True):
+        return self.kv.get(key)
+
+
+def test_verkey_from_state():
+    import json
+    from indy_plenum_amd.client_authn import nym_to_state_key
+    st = DictState()
+    st.kv[nym_to_state_key(kats.KAT2_IDR)] = json.dumps({'verkey': kats.KAT2_ABBR_VERKEY}).encode()
+    sa = CoreAuthNr(state=st)
+    assert sa.authenticate(kats.kat2_request(1)) == [kats.KAT2_IDR]
+
+
+# ---------------------------------------------------------------- batching
+def make_requests(n, seed=1):
+    """NYM-style requests with a mix of every outcome the chain can produce."""
+    r = random.Random(seed)
+    signers = [Signer(seed=bytes([k % 256, k // 256]) * 16) for k in range(12)]
+    sa = CoreAuthNr()
+    for s in signers[:10]:  # the last two are unknown identifiers
+        sa.addIdr(s.identifier, s.verkey)
+    reqs = []
+    for i in range(n):
+        s = r.choice(signers)
+        req = {'identifier': s.identifier, 'reqId': 1539648000000000 + i, 'protocolVersion': 2,
+               'operation': {'type': r.choice(['1', '1', '1', '0', '3', '101', '999']), 'dest': 'd%d' % i}}
+        kind = r.randrange(10)
+        if kind == 0:
+            req['signature'] = s.sign({**req, 'reqId': 0})  # wrong message
+        elif kind == 1:
+            req['signature'] = '0OIl'                       # not base58
+        elif kind == 2:
+            pass                                            # no signature at all
+        elif kind == 3:                                     # multi-signature, some wrong
+            ss = r.sample(signers, 3)
+            req['signatures'] = {x.identifier: (x.sign(req) if r.random() < 0.7 else x.sign({})) for x in ss}
+        elif kind == 4:
+            req['signature'] = s.sign(req)[:-2]             # truncated signature bytes
+        else:
+            req['signature'] = s.sign(req)
+        reqs.append(req)
+    return sa, reqs
+
+
+def outcome(f):
+    try:
+        return ("ok", f())
+    except Exception as ex:  # compare by type and args
+        return ("raise", type(ex).__name__, getattr(ex, "args", ()))
+
+
+def test_core_authenticate_batch_equals_sequential(cpu_checker):
+    sa, reqs = make_requests(300)
+    seq = [outcome(lambda r=r: sa.authenticate(r)) for r in reqs]
+    cpu_checker.clear()
+    bat = sa.authenticate_batch(reqs)
+    assert len(cpu_checker) == 1  # one device call for the whole batch
+    bat = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in bat]
+    assert bat == seq
+
+
+def test_req_authenticator_batch_equals_sequential(cpu_checker):
+    sa, reqs = make_requests(300, seed=2)
+
+    class ExtraAuthNr(CoreAuthNr):  # a plugin authenticator registered after the core one
+        write_types = frozenset({'101'})
+
+    extra = ExtraAuthNr()
+    for k, v in sa.clients.items():
+        extra.addIdr(k, v['verkey'])
+    ra = ReqAuthenticator()
+    ra.register_authenticator(sa)
+    ra.register_authenticator(extra)
+    assert ra.core_authenticator is sa
+    assert ra.get_authnr_by_type(ExtraAuthNr) is extra
+    seq = [outcome(lambda r=r: ra.authenticate(r)) for r in reqs]
+    cpu_checker.clear()
+    bat = ra.authenticate_batch(reqs)
+    assert len(cpu_checker) <= 2  # one device call per authenticator
+    bat = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in bat]
+    assert bat == seq
+    kinds = {o[0] if o[0] == "ok" else o[1] for o in seq}
+    assert {"ok", "NoAuthenticatorFound", "InsufficientCorrectSignatures", "InvalidSignatureFormat",
+            "MissingSignature", "UnknownIdentifier"} <= kinds
+
+
+def test_req_authenticator_query_and_no_authenticator():
+    ra = ReqAuthenticator()
+    with pytest.raises(RuntimeError):
+        ra.core_authenticator
+    sa = CoreAuthNr()
+    ra.register_authenticator(sa)
+    assert ra.authenticate({'operation': {'type': '3'}}) == set()
+    with pytest.raises(NoAuthenticatorFound):
+        ra.authenticate({'operation': {'type': '101'}, 'identifier': IDR, 'signature': 'x'})
+    res = ra.authenticate_batch([{'operation': {'type': '3'}}, {'operation': {'type': '101'}}])
+    assert res[0] == set() and isinstance(res[1], NoAuthenticatorFound)
