@@ -134,7 +134,14 @@ def main():
     prep_ms, main_ms = edv.profile_device(batch.d_sigs.ptr, batch.d_pks.ptr, batch.d_msgs.ptr, batch.d_off.ptr, n,
                                           batch.d_accept.ptr, dev, iters)
     ok = batch.accept()
-    all_ok = max_over_ranks(0.0 if ok.all() else 1.0) == 0.0
+    if dist is not None:
+        # untimed: gather every shard's accept bytes back into request order (RCCL all-gather)
+        from indy_plenum_amd import shard
+        import torch
+        full = shard.gather_accept(dist, ok, n * world, device=torch.device("cuda", local))
+        all_ok = bool(full.all())
+    else:
+        all_ok = bool(ok.all())
 
     if rank != 0:
         if dist is not None:

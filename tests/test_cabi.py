@@ -1,0 +1,62 @@
+"""The product C-ABI library builds, loads without a GPU and exports every
+symbol include/edv.h declares; without a GPU the shim fails loudly (no CPU
+fallback)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "edv.h")
+
+
+def declared():
+    src = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*|void)\s*\**\s*(edv_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_the_core_entry_points():
+    names = declared()
+    for need in ("edv_verify_batch", "edv_verify_batch_dev", "edv_version", "edv_last_error", "edv_device_count",
+                 "edv_sign_batch_dev", "edv_profile_batch_dev", "edv_time_batch_dev", "edv_set_chunk"):
+        assert need in names
+
+
+def test_library_exports_every_declared_symbol():
+    from indy_plenum_amd import edv
+    lib = edv.lib()
+    missing = [n for n in declared() if not hasattr(lib, n)]
+    assert missing == []
+    out = subprocess.check_output(["nm", "-D", "--defined-only", edv.LIB_PATH]).decode()
+    exported = set(re.findall(r" T (edv_\w+)$", out, re.M))
+    assert set(declared()) <= exported
+    assert edv.version().startswith("edv ") and "gfx950" in edv.version()
+
+
+def test_library_contains_gfx950_code_object():
+    from indy_plenum_amd import edv
+    blob = open(edv.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+    assert b"edv_main_kernel" in blob and b"edv_prep_kernel" in blob
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="a GPU is present")
+def test_no_gpu_means_loud_failure():
+    from indy_plenum_amd import edv
+    assert edv.device_count() == 0
+    with pytest.raises(edv.EdvUnavailable):
+        edv.verify_arrays(b"\0" * 64, b"\0" * 32, b"\0" * 16, np.array([0, 0], np.uint64))
+    with pytest.raises(edv.EdvUnavailable):
+        edv.open_batch([(b"\0" * 64, b"", b"\0" * 32)])
+
+
+def test_invalid_arguments_are_rejected_before_the_device():
+    from indy_plenum_amd import edv
+    with pytest.raises(ValueError):
+        edv.verify_arrays(b"\0" * 63, b"\0" * 32, b"", np.array([0, 0], np.uint64))
+    with pytest.raises(ValueError):
+        edv.open_batch([(b"\0" * 64, b"", b"\0" * 31)])
+    assert edv.open_batch([(b"\0" * 10, b"\0" * 10, b"\0" * 32)]) == [False]  # sm < 64: no device call
