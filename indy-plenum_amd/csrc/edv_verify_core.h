@@ -193,6 +193,18 @@ EDV_HD bool main_one(const uint32_t R[8], uint32_t hd[8], uint32_t sd[8], const 
   ge_p2 acc = ge_p2_identity();
 #pragma unroll 1
   for (int w = 63; w >= 0; --w) {
+    // table reads first, so their latency hides under this window's doublings
+    const int dA = int32_t(hd[7]) >> 28;
+    shl256<4>(hd);
+    const int ua = dA < 0 ? -dA : dA;
+    ge_cached c = at.load(ua == 0 ? 0 : ua - 1);
+    int dB = 0;
+    ge_precomp q;
+    if ((w & 1) == 0) {
+      dB = int32_t(sd[7]) >> 24;
+      shl256<8>(sd);
+      q = bt.entry(dB < 0 ? -dB : dB);
+    }
     ge_p3 p3;
     if (w == 63) {
       p3 = ge_p3_identity();
@@ -202,20 +214,12 @@ EDV_HD bool main_one(const uint32_t R[8], uint32_t hd[8], uint32_t sd[8], const 
       acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
       p3 = ge_p1p1_to_p3(ge_p2_dbl(acc));
     }
-    const int dA = int32_t(hd[7]) >> 28;
-    shl256<4>(hd);
-    const int ua = dA < 0 ? -dA : dA;
-    ge_cached c = at.load(ua == 0 ? 0 : ua - 1);
     if (ua == 0) c = ge_cached_identity();
     c = ge_cached_cneg(c, dA < 0);
     ge_p1p1 t = ge_add(p3, c);
     if ((w & 1) == 0) {
       p3 = ge_p1p1_to_p3(t);
-      const int dB = int32_t(sd[7]) >> 24;
-      shl256<8>(sd);
-      const int ub = dB < 0 ? -dB : dB;
-      const ge_precomp q = ge_precomp_cneg(bt.entry(ub), dB < 0);
-      t = ge_madd(p3, q);
+      t = ge_madd(p3, ge_precomp_cneg(q, dB < 0));
     }
     acc = ge_p1p1_to_p2(t);
   }
