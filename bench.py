@@ -88,12 +88,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # EDV_BENCH_ONE_DEVICE=1 (rehearsal on a 1-GPU box only): every rank uses device 0
+    # and gloo, since RCCL refuses two ranks on one GPU
+    one_dev = os.environ.get("EDV_BENCH_ONE_DEVICE") == "1"
     dist = None
     if world > 1:
         import torch
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")  # RCCL over xGMI
+        if one_dev:
+            tdist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            tdist.init_process_group("nccl")  # RCCL over xGMI
         dist = tdist
 
     def barrier():
@@ -104,11 +110,11 @@ def main():
         if dist is None:
             return x
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if one_dev else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    dev = local
+    dev = 0 if one_dev else local
     n = args.batch
     # this rank's shard of the request index space: [rank * n, (rank + 1) * n)
     batch = workload.DeviceBatch(n, device=dev, start=rank * n, msg_len=args.msg_len)
@@ -118,10 +124,16 @@ def main():
     ok = batch.accept()
     assert ok.all(), "warm-up verify rejected %d valid signatures" % int((ok == 0).sum())
 
+    # steps are enqueued back to back on the library's stream of this device
+    # (prep -> main per step, in order) and the timed region is closed by a
+    # device sync, so host launch latency does not sit between steps
+    s = edv.stream(dev)
+    edv.sync(dev)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        batch.verify()  # synchronous on the library stream of this device
+        batch.verify(stream=s)
+    edv.sync(dev)
     t1 = time.perf_counter()
     barrier()
     elapsed = max_over_ranks(t1 - t0)
@@ -138,7 +150,7 @@ def main():
         # untimed: gather every shard's accept bytes back into request order (RCCL all-gather)
         from indy_plenum_amd import shard
         import torch
-        full = shard.gather_accept(dist, ok, n * world, device=torch.device("cuda", local))
+        full = shard.gather_accept(dist, ok, n * world, device=None if one_dev else torch.device("cuda", local))
         all_ok = bool(full.all())
     else:
         all_ok = bool(ok.all())

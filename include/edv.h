@@ -100,6 +100,11 @@ int edv_set_chunk(int device, uint64_t chunk);
 int edv_sign_batch_dev(const uint8_t *d_seeds, const uint8_t *d_msgs, const uint64_t *d_msg_off, uint64_t msg_base,
                        uint64_t n, uint8_t *d_pks, uint8_t *d_sigs, int device, void *stream);
 
+/* The library's own HIP stream of `device` (so callers can enqueue several
+ * edv_*_dev calls asynchronously on it) and a wait for everything on it. */
+int edv_stream(int device, void **out);
+int edv_sync(int device);
+
 /* Number of visible gfx950 devices (0 if none). */
 int edv_device_count(void);
 

@@ -32,12 +32,12 @@ using namespace edv;
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kAWords = kAEntries * 40;   // cached point = 4 x 10 limbs
+constexpr int kAWords = kAEntries * 40;   // cached point = 4 x 10 limbs (360 words = 1,440 B)
 constexpr uint64_t kChunkDefault = uint64_t(1) << 18;  // signatures per prep/main launch pair
 
 // Per-chunk state handed from the prep kernel to the main kernel, SoA so every
 // wave-wide load/store touches 64 consecutive words:
-//   atab[320 * i + w]  word w (0..319) of signature i's 1..8 x (-A) table
+//   atab[360 * i + w]  word w (0..359) of signature i's 0..8 x (-A) table
 //   dig[w * cap + i]   w 0..7: packed radix-16 digits of h, 8..15: radix-256 digits of S
 //   alive[i]           1 if V2-V5 passed (the main kernel skips dead lanes' work)
 struct ChunkState {
@@ -61,8 +61,8 @@ struct VerifyArgs {
 };
 
 // ---------------------------------------------------------------- kernels
-// Per-signature A table in HBM, signature-major: signature i's 320 words are
-// contiguous at slot = atab + 320*i, so a lane's digit-dependent gather reads
+// Per-signature A table in HBM, signature-major: signature i's 360 words are
+// contiguous at slot = atab + 360*i, so a lane's digit-dependent gather reads
 // 160 contiguous bytes (10 x 16-byte loads) instead of touching one line per
 // word for every distinct digit in the wave (the word-major layout measured
 // 39 KB of L2-miss traffic per verify, 8x the useful bytes).
@@ -465,6 +465,29 @@ int edv_sign_batch_dev(const uint8_t* d_seeds, const uint8_t* d_msgs, const uint
                                                         reinterpret_cast<uint32_t*>(d_sigs), c->comb);
   HIPOK(hipGetLastError(), "sign launch");
   if (!stream) HIPOK(hipStreamSynchronize(s), "stream sync");
+  return 0;
+}
+
+int edv_stream(int device, void** out) {
+  g_err.clear();
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((err = ctx_init(*c, device))) return err;
+  *out = static_cast<void*>(c->stream);
+  return 0;
+}
+
+int edv_sync(int device) {
+  g_err.clear();
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((err = ctx_init(*c, device))) return err;
+  HIPOK(hipSetDevice(device), "hipSetDevice");
+  HIPOK(hipStreamSynchronize(c->stream), "stream sync");
   return 0;
 }
 

@@ -11,7 +11,7 @@
 
 namespace edv {
 
-constexpr int kAEntries = 8;   // per-lane table 1..8 x (-A), cached form
+constexpr int kAEntries = 9;   // per-lane table 0..8 x (-A), cached form (entry 0 = identity)
 constexpr int kBEntries = 129; // shared table 0..128 x B, affine precomp form
 constexpr int kBStride = 32;   // words per B entry (30 used; 128-byte aligned)
 
@@ -156,7 +156,7 @@ EDV_HD void btab_entry(int32_t* o, int j) {
 
 // Phase 1 of one signature (kernel edv_prep_kernel): strictness checks V2-V4,
 // decompression V5, h = SHA-512(R || A || M) mod L (V6, V7), digit recoding and
-// the 1..8 x (-A) table.  Returns false if the signature is already rejected
+// the 0..8 x (-A) table (entry 0 the identity, so a zero digit needs no select).  Returns false if the signature is already rejected
 // (then hd/sd/table are unspecified).  ATab provides store(e, cached).
 template <class ATab>
 EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen,
@@ -173,11 +173,12 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
   recode4(hd, h);
   recode8(sd, S);
   const ge_cached c1 = ge_p3_to_cached(nA);
-  at.store(0, c1);
+  at.store(0, ge_cached_identity());
+  at.store(1, c1);
   ge_p3 cur = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(nA)));
-  at.store(1, ge_p3_to_cached(cur));
+  at.store(2, ge_p3_to_cached(cur));
 #pragma unroll 1
-  for (int e = 2; e < kAEntries; e++) {
+  for (int e = 3; e < kAEntries; e++) {
     cur = ge_p1p1_to_p3(ge_add(cur, c1));
     at.store(e, ge_p3_to_cached(cur));
   }
@@ -196,8 +197,7 @@ EDV_HD bool main_one(const uint32_t R[8], uint32_t hd[8], uint32_t sd[8], const 
     // table reads first, so their latency hides under this window's doublings
     const int dA = int32_t(hd[7]) >> 28;
     shl256<4>(hd);
-    const int ua = dA < 0 ? -dA : dA;
-    ge_cached c = at.load(ua == 0 ? 0 : ua - 1);
+    ge_cached c = at.load(dA < 0 ? -dA : dA);
     int dB = 0;
     ge_precomp q;
     if ((w & 1) == 0) {
@@ -214,7 +214,6 @@ EDV_HD bool main_one(const uint32_t R[8], uint32_t hd[8], uint32_t sd[8], const 
       acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
       p3 = ge_p1p1_to_p3(ge_p2_dbl(acc));
     }
-    if (ua == 0) c = ge_cached_identity();
     c = ge_cached_cneg(c, dA < 0);
     ge_p1p1 t = ge_add(p3, c);
     if ((w & 1) == 0) {

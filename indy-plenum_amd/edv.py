@@ -68,6 +68,10 @@ def lib():
         h.edv_profile_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
         h.edv_profile_batch_dev.restype = ctypes.c_int
+        h.edv_stream.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        h.edv_stream.restype = ctypes.c_int
+        h.edv_sync.argtypes = [ctypes.c_int]
+        h.edv_sync.restype = ctypes.c_int
         h.edv_set_chunk.argtypes = [ctypes.c_int, u64]
         h.edv_set_chunk.restype = ctypes.c_int
         h.edv_device_count.argtypes = []
@@ -88,6 +92,18 @@ def version() -> str:
 
 def device_count() -> int:
     return lib().edv_device_count()
+
+
+def stream(device: int = 0) -> int:
+    """The library's HIP stream of `device` (for asynchronous edv_*_dev calls)."""
+    p = ctypes.c_void_p()
+    _check(lib().edv_stream(device, ctypes.byref(p)))
+    return p.value
+
+
+def sync(device: int = 0):
+    """Wait for everything enqueued on the library stream of `device`."""
+    _check(lib().edv_sync(device))
 
 
 def set_chunk(device: int, chunk: int):
