@@ -79,6 +79,7 @@ int edv_time_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_
  * Measurement helper: average per-launch milliseconds of the two kernels of
  * one batch (n <= chunk), each bracketed by HIP events on the kernel's stream:
  * prep (checks, decompression, SHA-512, table) and main (scalar mult, encode).
+ * The length-bucketing pass runs before each pair, outside the events.
  */
 int edv_profile_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
                           const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept, int device,

@@ -45,6 +45,7 @@ struct ChunkState {
   uint32_t* dig;
   uint8_t* alive;
   uint64_t cap;
+  const uint32_t* perm;   // slot j -> request base + perm[j] (length buckets); null = identity
 };
 
 struct VerifyArgs {
@@ -121,9 +122,9 @@ __device__ __forceinline__ void load_words(uint32_t* out, const uint32_t* p, int
 
 // Phase 1: V2-V7, digit recoding, the per-signature A table.
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 8))) void edv_prep_kernel(VerifyArgs a) {
-  const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;  // index within the chunk
+  const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;  // slot within the chunk
   if (j >= a.n) return;
-  const uint64_t i = a.base + j;
+  const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
   uint32_t R[8], S[8], A[8];
   load_words(R, a.sigs + 16 * i, 2);
   load_words(S, a.sigs + 16 * i + 8, 2);
@@ -152,7 +153,7 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   __syncthreads();
   const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= a.n || !a.st.alive[j]) return;
-  const uint64_t i = a.base + j;
+  const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
   uint32_t R[8], hd[8], sd[8];
   load_words(R, a.sigs + 16 * i, 2);
 #pragma unroll
@@ -203,6 +204,62 @@ __global__ void edv_comb_kernel(int32_t* out) {
   if (t < kCombRows * kBEntries) comb_entry(out + t * kBStride, t / kBEntries, t % kBEntries);
 }
 
+// ---- length buckets (config C4): group the chunk's requests by SHA-512 block
+// count so every wave of the prep kernel runs the same number of compression
+// rounds (a wave otherwise pays for its longest message).  Counting sort on
+// min(blocks, 63): histogram, then scatter with per-bucket atomic cursors; a
+// chunk whose requests all share one bucket keeps the identity order.
+constexpr int kBuckets = 64;
+__device__ __forceinline__ uint32_t sha_bucket(const uint64_t* off, uint64_t i) {
+  const uint64_t nb = (64 + (off[i + 1] - off[i]) + 17 + 127) / 128;
+  return nb < kBuckets - 1 ? uint32_t(nb) : uint32_t(kBuckets - 1);
+}
+// Histogram: per-workgroup counts in LDS, then one global add per non-empty
+// bucket per workgroup (a fixed-length batch would otherwise send every lane's
+// atomic to the same word).
+__global__ __launch_bounds__(kBlock) void edv_bucket_hist_kernel(const uint64_t* off, uint64_t base, uint64_t n,
+                                                                 uint32_t* hist) {
+  __shared__ uint32_t h[kBuckets];
+  if (threadIdx.x < kBuckets) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j < n) atomicAdd(&h[sha_bucket(off, base + j)], 1u);
+  __syncthreads();
+  if (threadIdx.x < kBuckets && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+// Scatter: bucket start offsets from the global histogram; each workgroup
+// reserves its range per bucket with one global add, then ranks its lanes
+// within the range through LDS.
+__global__ __launch_bounds__(kBlock) void edv_bucket_scatter_kernel(const uint64_t* off, uint64_t base, uint64_t n,
+                                                                    const uint32_t* hist, uint32_t* cursor,
+                                                                    uint32_t* perm) {
+  __shared__ uint32_t start[kBuckets], cnt[kBuckets], wbase[kBuckets];
+  __shared__ int nonempty;
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    int ne = 0;
+    for (int b = 0; b < kBuckets; b++) { start[b] = acc; acc += hist[b]; ne += hist[b] != 0; }
+    nonempty = ne;
+  }
+  if (threadIdx.x < kBuckets) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (nonempty <= 1) {
+    if (j < n) perm[j] = uint32_t(j);
+    return;
+  }
+  uint32_t b = 0, rank = 0;
+  if (j < n) {
+    b = sha_bucket(off, base + j);
+    rank = atomicAdd(&cnt[b], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kBuckets && cnt[threadIdx.x])
+    wbase[threadIdx.x] = start[threadIdx.x] + atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]);
+  __syncthreads();
+  if (j < n) perm[wbase[b] + rank] = uint32_t(j);
+}
+
 // j * B for j = 0..128 in affine precomp form, once per device
 __global__ void edv_btab_kernel(int32_t* out) {
   const int j = threadIdx.x + blockIdx.x * blockDim.x;
@@ -246,7 +303,8 @@ struct DevCtx {
   int32_t* btab = nullptr;
   int32_t* comb = nullptr;         // signer comb table, built on first edv_sign_* call
   uint64_t chunk = kChunkDefault;  // EDV_CHUNK overrides (tests exercise chunk seams)
-  DevBuf atab, dig, alive;  // ChunkState storage for `chunk` signatures (~350 MB at 2^18)
+  DevBuf atab, dig, alive;  // ChunkState storage for `chunk` signatures (~400 MB at 2^18)
+  DevBuf perm, bucket_ctr;  // length-bucket permutation of a chunk; histogram + cursors
   DevBuf sigs, pks, msgs, off, acc;
 };
 
@@ -276,7 +334,8 @@ int ctx_init(DevCtx& c, int dev) {
     const uint64_t v = strtoull(e, nullptr, 10);
     if (v >= kBlock && v <= (uint64_t(1) << 24)) c.chunk = (v / kBlock) * kBlock;
   }
-  if (c.atab.ensure(c.chunk * kAWords * 4) || c.dig.ensure(c.chunk * 16 * 4) || c.alive.ensure(c.chunk))
+  if (c.atab.ensure(c.chunk * kAWords * 4) || c.dig.ensure(c.chunk * 16 * 4) || c.alive.ensure(c.chunk) ||
+      c.perm.ensure(c.chunk * 4) || c.bucket_ctr.ensure(2 * kBuckets * 4))
     return EDV_E_OOM;
   HIPOK(hipMalloc(&c.btab, kBEntries * kBStride * 4), "hipMalloc btab");
   edv_btab_kernel<<<(kBEntries + 63) / 64, 64, 0, c.stream>>>(c.btab);
@@ -295,9 +354,11 @@ DevCtx* get_ctx(int dev, int* err) {
 }
 
 // launch on ctx stream or the given stream; caller holds c.mu.  The batch is
-// walked in chunks of kChunk signatures: prep kernel, then main kernel.
+// walked in chunks of c.chunk signatures: [length buckets,] prep kernel, main kernel.
 int launch(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_off,
-           uint64_t msg_base, uint64_t n, uint8_t* d_accept, hipStream_t s) {
+           uint64_t msg_base, uint64_t n, uint8_t* d_accept, hipStream_t s, bool bucket = true) {
+  static const bool no_bucket = getenv("EDV_NO_BUCKET") != nullptr;  // A/B measurement knob
+  bucket = bucket && !no_bucket;
   VerifyArgs va;
   va.sigs = reinterpret_cast<const uint32_t*>(d_sigs);
   va.pks = reinterpret_cast<const uint32_t*>(d_pks);
@@ -306,12 +367,20 @@ int launch(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t
   va.msg_base = msg_base;
   va.accept = d_accept;
   va.st = ChunkState{static_cast<int32_t*>(c.atab.p), static_cast<uint32_t*>(c.dig.p),
-                     static_cast<uint8_t*>(c.alive.p), c.chunk};
+                     static_cast<uint8_t*>(c.alive.p), c.chunk, bucket ? static_cast<uint32_t*>(c.perm.p) : nullptr};
   va.btab = c.btab;
+  uint32_t* hist = static_cast<uint32_t*>(c.bucket_ctr.p);
   for (uint64_t base = 0; base < n; base += c.chunk) {
     va.base = base;
     va.n = (n - base) < c.chunk ? (n - base) : c.chunk;
     const unsigned blocks = unsigned((va.n + kBlock - 1) / kBlock);
+    if (bucket) {
+      HIPOK(hipMemsetAsync(hist, 0, 2 * kBuckets * 4, s), "memset buckets");
+      edv_bucket_hist_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, base, va.n, hist);
+      edv_bucket_scatter_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, base, va.n, hist, hist + kBuckets,
+                                                                       static_cast<uint32_t*>(c.perm.p));
+      HIPOK(hipGetLastError(), "bucket launch");
+    }
     edv_prep_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
     HIPOK(hipGetLastError(), "prep launch");
     edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
@@ -339,9 +408,15 @@ int run_shard(int dev, const uint8_t* sigs, const uint8_t* pks, const uint8_t* m
   HIPOK(hipMemcpyAsync(c->pks.p, pks + 32 * lo, n * 32, hipMemcpyHostToDevice, c->stream), "h2d pks");
   if (mbytes) HIPOK(hipMemcpyAsync(c->msgs.p, msgs + mbase, mbytes, hipMemcpyHostToDevice, c->stream), "h2d msgs");
   HIPOK(hipMemcpyAsync(c->off.p, off + lo, (n + 1) * 8, hipMemcpyHostToDevice, c->stream), "h2d off");
+  // bucket by SHA block count only when the shard's messages differ in block count
+  bool varied = false;
+  {
+    const uint64_t nb0 = (64 + off[lo + 1] - off[lo] + 17 + 127) / 128;
+    for (uint64_t i = lo + 1; i < hi && !varied; i++) varied = (64 + off[i + 1] - off[i] + 17 + 127) / 128 != nb0;
+  }
   if ((err = launch(*c, static_cast<uint8_t*>(c->sigs.p), static_cast<uint8_t*>(c->pks.p),
                     static_cast<uint8_t*>(c->msgs.p), static_cast<uint64_t*>(c->off.p), mbase, n,
-                    static_cast<uint8_t*>(c->acc.p), c->stream)))
+                    static_cast<uint8_t*>(c->acc.p), c->stream, varied)))
     return err;
   HIPOK(hipMemcpyAsync(accept + lo, c->acc.p, n, hipMemcpyDeviceToHost, c->stream), "d2h accept");
   HIPOK(hipStreamSynchronize(c->stream), "stream sync");
@@ -503,7 +578,8 @@ int edv_set_chunk(int device, uint64_t chunk) {
   if (chunk == 0) chunk = kChunkDefault;
   if (chunk < kBlock || chunk > (uint64_t(1) << 24)) return set_err(EDV_E_ARG, "chunk out of range");
   c->chunk = (chunk / kBlock) * kBlock;
-  if (c->atab.ensure(c->chunk * kAWords * 4) || c->dig.ensure(c->chunk * 16 * 4) || c->alive.ensure(c->chunk))
+  if (c->atab.ensure(c->chunk * kAWords * 4) || c->dig.ensure(c->chunk * 16 * 4) || c->alive.ensure(c->chunk) ||
+      c->perm.ensure(c->chunk * 4))
     return EDV_E_OOM;
   return 0;
 }
@@ -527,15 +603,24 @@ int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uin
   va.msg_base = msg_base;
   va.accept = d_accept;
   va.st = ChunkState{static_cast<int32_t*>(c->atab.p), static_cast<uint32_t*>(c->dig.p),
-                     static_cast<uint8_t*>(c->alive.p), c->chunk};
+                     static_cast<uint8_t*>(c->alive.p), c->chunk, static_cast<uint32_t*>(c->perm.p)};
   va.btab = c->btab;
   va.base = 0;
+  uint32_t* hist = static_cast<uint32_t*>(c->bucket_ctr.p);
+  const bool bucket = getenv("EDV_NO_BUCKET") == nullptr;
+  if (!bucket) va.st.perm = nullptr;
   va.n = n;
   const unsigned blocks = unsigned((n + kBlock - 1) / kBlock);
   hipEvent_t ev[3];
   for (auto& e : ev) HIPOK(hipEventCreate(&e), "event");
   float tp = 0, tm = 0;
   for (int it = 0; it < iters; it++) {
+    if (bucket) {
+      HIPOK(hipMemsetAsync(hist, 0, 2 * kBuckets * 4, c->stream), "memset buckets");
+      edv_bucket_hist_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(d_msg_off, 0, n, hist);
+      edv_bucket_scatter_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(d_msg_off, 0, n, hist, hist + kBuckets,
+                                                                               static_cast<uint32_t*>(c->perm.p));
+    }
     HIPOK(hipEventRecord(ev[0], c->stream), "record");
     edv_prep_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(va);
     HIPOK(hipEventRecord(ev[1], c->stream), "record");

@@ -82,9 +82,11 @@ def test_variable_length_c4_vs_libsodium():
     assert np.array_equal(got, checker(sigs, pks, msgs, off))
 
 
-def test_chunk_seams():
-    """Batches spanning several prep/main chunk pairs (chunk forced small)."""
-    sigs, pks, msgs, off = orc.corpus(0x5EA, 0, 5000, mode=0, invalid_permille=200)
+@pytest.mark.parametrize("mode", [0, 1])
+def test_chunk_seams(mode):
+    """Batches spanning several prep/main chunk pairs (chunk forced small); mode 1
+    (200..4096 B) also exercises the per-chunk SHA length buckets."""
+    sigs, pks, msgs, off = orc.corpus(0x5EA + mode, 0, 5000, mode=mode, invalid_permille=200)
     want = checker(sigs, pks, msgs, off)
     try:
         for chunk in (256, 768, 4096):
