@@ -501,8 +501,37 @@ EDV_HD void sc_reduce(uint32_t out[8], const uint32_t in[16]) {
 }
 
 // ------------------------------------------------------------------ SHA-512 (V6)
-EDV_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate as two 32-bit funnel shifts (v_alignbit_b32 each): the plain
+// (x >> n) | (x << 64-n) form compiles to two 64-bit shifts and two ORs.
+EDV_HD uint32_t funnel32(uint32_t hi, uint32_t lo, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(hi, lo, n);  // opaque: keeps one v_alignbit_b32 per half
+#else
+  return uint32_t(((uint64_t(hi) << 32) | lo) >> n);
+#endif
+}
+struct u32x2 { uint32_t lo, hi; };
+EDV_HD uint64_t pack64(uint32_t lo, uint32_t hi) { return __builtin_bit_cast(uint64_t, u32x2{lo, hi}); }
+EDV_HD uint64_t rotr64(uint64_t x, int n) {
+  const u32x2 p = __builtin_bit_cast(u32x2, x);
+  // rotr by n < 32: lo' = (hi:lo) >> n, hi' = (lo:hi) >> n; n >= 32 swaps the halves first
+  if (n >= 32) return pack64(funnel32(p.lo, p.hi, n - 32), funnel32(p.hi, p.lo, n - 32));
+  return pack64(funnel32(p.hi, p.lo, n), funnel32(p.lo, p.hi, n));
+}
 
+EDV_HD void sha512_round(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t& e, uint64_t& f, uint64_t& g,
+                         uint64_t& h, uint64_t kw) {
+  const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+  const uint64_t ch = (e & f) ^ (~e & g);
+  const uint64_t t1 = h + S1 + ch + kw;
+  const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+  const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+  d += t1;
+  h = t1 + S0 + mj;
+}
+// One compression.  Rounds run 16 at a time with the register rotation
+// unrolled, so every W index is a compile-time constant (no dynamic register
+// indexing) while the code stays one 16-round body.
 EDV_HD void sha512_compress(uint64_t H[8], uint64_t W[16]) {
   const uint64_t K[80] = {
       0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
@@ -526,24 +555,33 @@ EDV_HD void sha512_compress(uint64_t H[8], uint64_t W[16]) {
       0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
       0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
   uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+#pragma unroll 1
+  for (int r = 0; r < 80; r += 16) {
+    if (r > 0) {
 #pragma unroll
-  for (int t = 0; t < 80; t++) {
-    uint64_t w;
-    if (t < 16) {
-      w = W[t];
-    } else {
-      const uint64_t w15 = W[(t - 15) & 15], w2 = W[(t - 2) & 15];
-      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-      w = W[t & 15] + s0 + W[(t - 7) & 15] + s1;
-      W[t & 15] = w;
+      for (int t = 0; t < 16; t++) {
+        const uint64_t w15 = W[(t + 1) & 15], w2 = W[(t + 14) & 15];
+        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
+        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+        W[t] += s0 + W[(t + 9) & 15] + s1;
+      }
     }
-    const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-    const uint64_t ch = (e & f) ^ (~e & g);
-    const uint64_t t1 = h + S1 + ch + K[t] + w;
-    const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-    const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
-    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    sha512_round(a, b, c, d, e, f, g, h, K[r + 0] + W[0]);
+    sha512_round(h, a, b, c, d, e, f, g, K[r + 1] + W[1]);
+    sha512_round(g, h, a, b, c, d, e, f, K[r + 2] + W[2]);
+    sha512_round(f, g, h, a, b, c, d, e, K[r + 3] + W[3]);
+    sha512_round(e, f, g, h, a, b, c, d, K[r + 4] + W[4]);
+    sha512_round(d, e, f, g, h, a, b, c, K[r + 5] + W[5]);
+    sha512_round(c, d, e, f, g, h, a, b, K[r + 6] + W[6]);
+    sha512_round(b, c, d, e, f, g, h, a, K[r + 7] + W[7]);
+    sha512_round(a, b, c, d, e, f, g, h, K[r + 8] + W[8]);
+    sha512_round(h, a, b, c, d, e, f, g, K[r + 9] + W[9]);
+    sha512_round(g, h, a, b, c, d, e, f, K[r + 10] + W[10]);
+    sha512_round(f, g, h, a, b, c, d, e, K[r + 11] + W[11]);
+    sha512_round(e, f, g, h, a, b, c, d, K[r + 12] + W[12]);
+    sha512_round(d, e, f, g, h, a, b, c, K[r + 13] + W[13]);
+    sha512_round(c, d, e, f, g, h, a, b, K[r + 14] + W[14]);
+    sha512_round(b, c, d, e, f, g, h, a, K[r + 15] + W[15]);
   }
   H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
 }
