@@ -35,6 +35,37 @@ from indy_plenum_amd import edv, workload  # noqa: E402
 MAIN_OPS = (2737 + 267) * 64
 
 
+def kernel_source_hash():
+    """SHA-256 over the HIP sources of libedv.so (ties a committed PMC summary to the code it measured)."""
+    import hashlib
+    d = os.path.join(ROOT, "indy-plenum_amd", "csrc")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".h")):
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()
+
+
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_hbm_latest.json")
+
+
+def measured_traffic(kernel, batch, msg_len):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (tools/pmc_summary.py), only if it was measured on these exact kernel sources
+    at the default C2 shape; else None."""
+    if batch != 65536 or msg_len != 256 or not os.path.exists(PMC_SUMMARY):
+        return None, "no PMC summary for this shape"
+    with open(PMC_SUMMARY) as f:
+        s = json.load(f)
+    if s.get("kernel_source_sha256") != kernel_source_hash():
+        return None, "PMC summary is stale (kernel sources changed since it was measured)"
+    k = s["kernels"].get(kernel)
+    if not k:
+        return None, "kernel not in PMC summary"
+    return k["hbm_bytes_per_launch"], "profiles/pmc_hbm_latest.json: (2 x FETCH_SIZE + WRITE_SIZE) KiB per launch"
+
+
 def w_total(m):
     return 217600 + 5500 * -(-(m + 81) // 128)
 
@@ -160,6 +191,7 @@ def main():
             dist.destroy_process_group()
         return
     achieved = MAIN_OPS * n / (main_ms * 1e-3)
+    traffic, traffic_src = measured_traffic("edv_main_kernel", n, args.msg_len)
     whole = w_total(args.msg_len) * n / ((prep_ms + main_ms) * 1e-3)
     out = {
         "metric": "Ed25519 verifies/sec (256B msgs) + % of INT32 VALU peak",
@@ -179,7 +211,8 @@ def main():
                    "batch_per_gpu": n, "msg_len": args.msg_len, "parallelism": "shard-by-request-index x%d" % world},
         "roofline": {"bound": "valu_int32", "kernel": "edv_main_kernel",
                      "achieved": achieved / 1e12, "peak": PEAK_INT32 / 1e12, "unit": "TOP/s",
-                     "frac": achieved / PEAK_INT32, "traffic": None,
+                     "frac": achieved / PEAK_INT32, "traffic": traffic, "traffic_unit": "bytes/launch",
+                     "traffic_source": traffic_src, "algorithmic_bytes": (64 + 32 + args.msg_len + 8 + 1) * n,
                      "ops_per_launch": MAIN_OPS * n, "kernel_ms": main_ms, "prep_kernel_ms": prep_ms,
                      "whole_path_frac": whole / PEAK_INT32},
         "all_accepted": bool(all_ok),
