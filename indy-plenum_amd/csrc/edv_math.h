@@ -99,6 +99,50 @@ EDV_HD fe fe_carry64(int64_t h0, int64_t h1, int64_t h2, int64_t h3, int64_t h4,
              int32_t(h7), int32_t(h8), int32_t(h9)}};
 }
 
+// Rounding bias of column k (2^(W_k - 1)).  The product kernels START their
+// column accumulators at this value (it rides in as the addend of the first
+// v_mad_i64_i32), so each first-pass carry step below is one 64-bit shift, one
+// 64-bit add and a mask: the separate 64-bit bias add of carry_step is gone
+// (10 of the 12 steps).  On the device the bias is read from constant memory:
+// as a literal, LLVM's reassociation moves it to the END of the column sum and
+// emits exactly the 64-bit add this saves (main kernel: 1,383 -> 704
+// v_lshl_add_u64, 11.3k -> 10.7k instructions, 204 -> 193 VGPRs).
+EDV_HD constexpr int64_t col_bias(int k) { return (k & 1) ? (int64_t(1) << 24) : (int64_t(1) << 25); }
+#if defined(__HIP_DEVICE_COMPILE__)
+__constant__ int64_t c_col_bias[2] = {int64_t(1) << 25, int64_t(1) << 24};
+EDV_HD int64_t bias_reg(int k) { return c_col_bias[k & 1]; }
+#else
+EDV_HD int64_t bias_reg(int k) { return col_bias(k); }
+#endif
+template <int W>
+EDV_HD int32_t carry_biased(int64_t t, int64_t& next) {
+  next += t >> W;  // arithmetic shift of the biased column = rounded carry
+  return int32_t(uint32_t(t) & ((1u << W) - 1)) - (1 << (W - 1));
+}
+// fe_carry64 for columns that carry their col_bias (same carry order, same
+// rounding, hence the same output bounds).  A column that has already been
+// reduced to a limb and then receives a carry (h4, and h0 after the 19-fold)
+// is unbiased, so its second step is an ordinary carry_step.
+EDV_HD fe fe_carry64_biased(int64_t h0, int64_t h1, int64_t h2, int64_t h3, int64_t h4, int64_t h5, int64_t h6,
+                            int64_t h7, int64_t h8, int64_t h9) {
+  h0 = carry_biased<26>(h0, h1);
+  h4 = carry_biased<26>(h4, h5);
+  h1 = carry_biased<25>(h1, h2);
+  h5 = carry_biased<25>(h5, h6);
+  h2 = carry_biased<26>(h2, h3);
+  h6 = carry_biased<26>(h6, h7);
+  h3 = carry_biased<25>(h3, h4);
+  h7 = carry_biased<25>(h7, h8);
+  h4 = carry_step<26>(h4, h5);
+  h8 = carry_biased<26>(h8, h9);
+  int64_t c9 = 0;
+  h9 = carry_biased<25>(h9, c9);
+  h0 += c9 * 19;
+  h0 = carry_step<26>(h0, h1);
+  return fe{{int32_t(h0), int32_t(h1), int32_t(h2), int32_t(h3), int32_t(h4), int32_t(h5), int32_t(h6),
+             int32_t(h7), int32_t(h8), int32_t(h9)}};
+}
+
 // h = f * g.  Column k collects f_i g_j with i + j = k (weight 1) or k + 10
 // (weight 19 via the pre-multiplied g_j*19); odd*odd products carry an extra 2
 // because of the 26/25 limb alternation (applied to the odd f_i when k is even).
@@ -128,21 +172,24 @@ EDV_HD fe fe_mul(const fe& f, const fe& g) {
       const int j = k - i;
       const int32_t a = ((k & 1) == 0) ? f2[i] : f.v[i];
       const int32_t b = (j >= 0) ? g.v[j] : g19[j + 10];
-      acc += int64_t(a) * int64_t(b);
+      acc = (i == 0) ? int64_t(a) * int64_t(b) + bias_reg(k) : acc + int64_t(a) * int64_t(b);
     }
     h[k] = acc;
   }
-  const fe r = fe_carry64(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
+  const fe r = fe_carry64_biased(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
   sched_fence();
   return r;
 }
 
 // Squaring columns (55 products): term f_i f_j (i <= j) with multiplier
-// (i<j ? 2 : 1) * (i,j both odd ? 2 : 1) * (i+j >= 10 ? 19 : 1), split between
-// the two operands so each stays inside int32 under the mul input bounds.
+// (i<j ? 2 : 1) * (i,j both odd ? 2 : 1) * (i+j >= 10 ? 19 : 1) (* 2 for
+// DOUBLE, i.e. 2 f^2), split between the two operands so each stays inside
+// int32 under the mul input bounds.  Columns start at col_bias.
+template <bool DOUBLE>
 EDV_HD void fe_sq_cols(const fe& f, int64_t h[10]) {
+  bool first[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) h[k] = 0;
+  for (int k = 0; k < 10; k++) first[k] = true;
 #pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
@@ -164,17 +211,23 @@ EDV_HD void fe_sq_cols(const fe& f, int64_t h[10]) {
         else if (i & 1) ma = 38;                // i odd, j even: 38 on f_i
         else mb = 19;                           // both even, i < j: 2 on f_i, 19 on f_j
       }
+      // the extra 2 of 2 f^2 goes on the operand without the 19 (at most 4 f_i then)
+      if (DOUBLE) {
+        if (ma <= 2) ma *= 2;
+        else mb *= 2;
+      }
       a = a * ma;
       b = b * mb;
-      h[k] += int64_t(a) * int64_t(b);
+      h[k] = first[k] ? int64_t(a) * int64_t(b) + bias_reg(k) : h[k] + int64_t(a) * int64_t(b);
+      first[k] = false;
     }
   }
 }
 EDV_HD fe fe_sq(const fe& f) {
   sched_fence();
   int64_t h[10];
-  fe_sq_cols(f, h);
-  const fe r = fe_carry64(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
+  fe_sq_cols<false>(f, h);
+  const fe r = fe_carry64_biased(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
   sched_fence();
   return r;
 }
@@ -182,10 +235,8 @@ EDV_HD fe fe_sq(const fe& f) {
 EDV_HD fe fe_sq2(const fe& f) {
   sched_fence();
   int64_t h[10];
-  fe_sq_cols(f, h);
-#pragma unroll
-  for (int k = 0; k < 10; k++) h[k] += h[k];
-  const fe r = fe_carry64(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
+  fe_sq_cols<true>(f, h);
+  const fe r = fe_carry64_biased(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
   sched_fence();
   return r;
 }

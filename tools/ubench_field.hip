@@ -78,7 +78,7 @@ __device__ __forceinline__ fe sq_v(const fe& f) {
   if constexpr (V == 0) return fe_sq(f);
   sched_fence();
   int64_t h[10];
-  fe_sq_cols(f, h);
+  fe_sq_cols<false>(f, h);
   fe r = (V == 1) ? carry64_b(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9])
                   : carry64_c(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
   sched_fence();
