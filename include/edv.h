@@ -67,6 +67,24 @@ int edv_verify_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uint
                          int device, void *stream);
 
 /*
+ * Pipelined submission of device-resident batches (a continuous stream of
+ * client batches, e.g. one per Node prod): enqueues the batch and returns
+ * without waiting.  Consecutive submissions alternate between two internal
+ * state sets, with the prep kernel (checks, decompression, SHA-512, table) of
+ * batch k+1 on one library stream and the main kernel (scalar multiplication,
+ * encode) of batch k on another, so both run on the SIMDs at once.  Work
+ * already queued on the library stream (edv_stream) is ordered before the
+ * batch; inputs must stay unchanged and each batch's d_accept must not be
+ * reused or read until edv_pipeline_sync(device) returns.  Same verdicts as
+ * edv_verify_batch_dev.
+ */
+int edv_verify_batch_dev_pipelined(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
+                                   const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept,
+                                   int device);
+/* Wait until every pipelined batch submitted on `device` has its verdicts. */
+int edv_pipeline_sync(int device);
+
+/*
  * Measurement helper for bench.py: launches the verify kernel `iters` times
  * on device-resident inputs between two HIP events recorded on the kernel's
  * own stream and returns the elapsed milliseconds of the whole region.

@@ -295,6 +295,18 @@ struct DevBuf {
   }
 };
 
+// One set of per-chunk state buffers (ChunkState storage + bucket permutation).
+struct ChunkBufs {
+  DevBuf atab, dig, alive;  // ChunkState storage for `chunk` signatures (~400 MB at 2^18)
+  DevBuf perm, bucket_ctr;  // length-bucket permutation of a chunk; histogram + cursors
+  int ensure(uint64_t chunk) {
+    if (atab.ensure(chunk * kAWords * 4) || dig.ensure(chunk * 16 * 4) || alive.ensure(chunk) ||
+        perm.ensure(chunk * 4) || bucket_ctr.ensure(2 * kBuckets * 4))
+      return EDV_E_OOM;
+    return 0;
+  }
+};
+
 struct DevCtx {
   std::mutex mu;
   bool ready = false;
@@ -303,9 +315,18 @@ struct DevCtx {
   int32_t* btab = nullptr;
   int32_t* comb = nullptr;         // signer comb table, built on first edv_sign_* call
   uint64_t chunk = kChunkDefault;  // EDV_CHUNK overrides (tests exercise chunk seams)
-  DevBuf atab, dig, alive;  // ChunkState storage for `chunk` signatures (~400 MB at 2^18)
-  DevBuf perm, bucket_ctr;  // length-bucket permutation of a chunk; histogram + cursors
+  ChunkBufs st;                    // state of the ordinary (one stream) path
   DevBuf sigs, pks, msgs, off, acc;
+  // Pipelined submission (edv_verify_batch_dev_pipelined): two state sets, a
+  // prep stream and a main stream, so the prep kernel of batch k+1 runs on the
+  // SIMDs beside the main kernel of batch k.  prep_done[b] orders main after its
+  // prep; main_done[b] keeps the next prep from overwriting state set b early.
+  bool pipe_ready = false;
+  ChunkBufs pst[2];
+  hipStream_t sp = nullptr, sm = nullptr;
+  hipEvent_t prep_done[2] = {nullptr, nullptr}, main_done[2] = {nullptr, nullptr}, inputs_ready = nullptr;
+  bool pending[2] = {false, false};
+  int next = 0;
 };
 
 std::mutex g_mu;
@@ -334,9 +355,7 @@ int ctx_init(DevCtx& c, int dev) {
     const uint64_t v = strtoull(e, nullptr, 10);
     if (v >= kBlock && v <= (uint64_t(1) << 24)) c.chunk = (v / kBlock) * kBlock;
   }
-  if (c.atab.ensure(c.chunk * kAWords * 4) || c.dig.ensure(c.chunk * 16 * 4) || c.alive.ensure(c.chunk) ||
-      c.perm.ensure(c.chunk * 4) || c.bucket_ctr.ensure(2 * kBuckets * 4))
-    return EDV_E_OOM;
+  if (c.st.ensure(c.chunk)) return EDV_E_OOM;
   HIPOK(hipMalloc(&c.btab, kBEntries * kBStride * 4), "hipMalloc btab");
   edv_btab_kernel<<<(kBEntries + 63) / 64, 64, 0, c.stream>>>(c.btab);
   HIPOK(hipGetLastError(), "btab launch");
@@ -353,12 +372,8 @@ DevCtx* get_ctx(int dev, int* err) {
   return g_ctx[dev];
 }
 
-// launch on ctx stream or the given stream; caller holds c.mu.  The batch is
-// walked in chunks of c.chunk signatures: [length buckets,] prep kernel, main kernel.
-int launch(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_off,
-           uint64_t msg_base, uint64_t n, uint8_t* d_accept, hipStream_t s, bool bucket = true) {
-  static const bool no_bucket = getenv("EDV_NO_BUCKET") != nullptr;  // A/B measurement knob
-  bucket = bucket && !no_bucket;
+VerifyArgs make_args(const DevCtx& c, ChunkBufs& b, const uint8_t* d_sigs, const uint8_t* d_pks,
+                     const uint8_t* d_msgs, const uint64_t* d_off, uint64_t msg_base, uint8_t* d_accept, bool bucket) {
   VerifyArgs va;
   va.sigs = reinterpret_cast<const uint32_t*>(d_sigs);
   va.pks = reinterpret_cast<const uint32_t*>(d_pks);
@@ -366,25 +381,100 @@ int launch(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t
   va.off = d_off;
   va.msg_base = msg_base;
   va.accept = d_accept;
-  va.st = ChunkState{static_cast<int32_t*>(c.atab.p), static_cast<uint32_t*>(c.dig.p),
-                     static_cast<uint8_t*>(c.alive.p), c.chunk, bucket ? static_cast<uint32_t*>(c.perm.p) : nullptr};
+  va.st = ChunkState{static_cast<int32_t*>(b.atab.p), static_cast<uint32_t*>(b.dig.p), static_cast<uint8_t*>(b.alive.p),
+                     c.chunk, bucket ? static_cast<uint32_t*>(b.perm.p) : nullptr};
   va.btab = c.btab;
-  uint32_t* hist = static_cast<uint32_t*>(c.bucket_ctr.p);
+  va.base = 0;
+  va.n = 0;
+  return va;
+}
+
+// [length buckets,] prep kernel of one chunk on stream s
+int launch_prep(ChunkBufs& b, const VerifyArgs& va, const uint64_t* d_off, bool bucket, hipStream_t s) {
+  const unsigned blocks = unsigned((va.n + kBlock - 1) / kBlock);
+  if (bucket) {
+    uint32_t* hist = static_cast<uint32_t*>(b.bucket_ctr.p);
+    HIPOK(hipMemsetAsync(hist, 0, 2 * kBuckets * 4, s), "memset buckets");
+    edv_bucket_hist_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, va.base, va.n, hist);
+    edv_bucket_scatter_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, va.base, va.n, hist, hist + kBuckets,
+                                                                     static_cast<uint32_t*>(b.perm.p));
+    HIPOK(hipGetLastError(), "bucket launch");
+  }
+  edv_prep_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
+  HIPOK(hipGetLastError(), "prep launch");
+  return 0;
+}
+int launch_main(const VerifyArgs& va, hipStream_t s) {
+  const unsigned blocks = unsigned((va.n + kBlock - 1) / kBlock);
+  edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
+  HIPOK(hipGetLastError(), "main launch");
+  return 0;
+}
+
+static bool bucketing_enabled(bool want) {
+  static const bool no_bucket = getenv("EDV_NO_BUCKET") != nullptr;  // A/B measurement knob
+  return want && !no_bucket;
+}
+
+// Ordinary path: launch on ctx stream or the given stream; caller holds c.mu.
+// The batch is walked in chunks of c.chunk signatures: [length buckets,] prep
+// kernel, main kernel, all in stream order.
+int launch(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_off,
+           uint64_t msg_base, uint64_t n, uint8_t* d_accept, hipStream_t s, bool bucket = true) {
+  bucket = bucketing_enabled(bucket);
+  if (c.pipe_ready) {  // state set 0 of the pipeline is separate, but drain it so results stay ordered
+    HIPOK(hipStreamSynchronize(c.sp), "pipeline sync");
+    HIPOK(hipStreamSynchronize(c.sm), "pipeline sync");
+  }
+  VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, msg_base, d_accept, bucket);
+  int err;
   for (uint64_t base = 0; base < n; base += c.chunk) {
     va.base = base;
     va.n = (n - base) < c.chunk ? (n - base) : c.chunk;
-    const unsigned blocks = unsigned((va.n + kBlock - 1) / kBlock);
-    if (bucket) {
-      HIPOK(hipMemsetAsync(hist, 0, 2 * kBuckets * 4, s), "memset buckets");
-      edv_bucket_hist_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, base, va.n, hist);
-      edv_bucket_scatter_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, base, va.n, hist, hist + kBuckets,
-                                                                       static_cast<uint32_t*>(c.perm.p));
-      HIPOK(hipGetLastError(), "bucket launch");
-    }
-    edv_prep_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
-    HIPOK(hipGetLastError(), "prep launch");
-    edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
-    HIPOK(hipGetLastError(), "main launch");
+    if ((err = launch_prep(c.st, va, d_off, bucket, s)) || (err = launch_main(va, s))) return err;
+  }
+  return 0;
+}
+
+int pipe_init(DevCtx& c) {
+  if (c.pipe_ready) return 0;
+  if (c.pst[0].ensure(c.chunk) || c.pst[1].ensure(c.chunk)) return EDV_E_OOM;
+  HIPOK(hipStreamCreateWithFlags(&c.sp, hipStreamNonBlocking), "hipStreamCreate");
+  HIPOK(hipStreamCreateWithFlags(&c.sm, hipStreamNonBlocking), "hipStreamCreate");
+  for (int b = 0; b < 2; b++) {
+    HIPOK(hipEventCreateWithFlags(&c.prep_done[b], hipEventDisableTiming), "event");
+    HIPOK(hipEventCreateWithFlags(&c.main_done[b], hipEventDisableTiming), "event");
+  }
+  HIPOK(hipEventCreateWithFlags(&c.inputs_ready, hipEventDisableTiming), "event");
+  c.pipe_ready = true;
+  return 0;
+}
+
+// Pipelined path: chunk k's prep goes on stream sp into state set k%2 (after
+// the main kernel that last read that set), its main on stream sm after that
+// prep.  Work already queued on the library stream (e.g. the batch signer)
+// is ordered before the first prep.  Caller holds c.mu.
+int launch_pipelined(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
+                     const uint64_t* d_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept) {
+  int err;
+  if ((err = pipe_init(c))) return err;
+  const bool bucket = bucketing_enabled(true);
+  HIPOK(hipEventRecord(c.inputs_ready, c.stream), "record");
+  HIPOK(hipStreamWaitEvent(c.sp, c.inputs_ready, 0), "wait");
+  for (uint64_t base = 0; base < n; base += c.chunk) {
+    const int b = c.next;
+    c.next ^= 1;
+    ChunkBufs& cb = c.pst[b];
+    VerifyArgs va = make_args(c, cb, d_sigs, d_pks, d_msgs, d_off, msg_base, d_accept, bucket);
+    va.base = base;
+    va.n = (n - base) < c.chunk ? (n - base) : c.chunk;
+    if (c.pending[b]) HIPOK(hipStreamWaitEvent(c.sp, c.main_done[b], 0), "wait");
+    if ((err = launch_prep(cb, va, d_off, bucket, c.sp))) return err;
+    HIPOK(hipEventRecord(c.prep_done[b], c.sp), "record");
+    HIPOK(hipStreamWaitEvent(c.sm, c.prep_done[b], 0), "wait");
+    if ((err = launch_main(va, c.sm))) return err;
+    HIPOK(hipEventRecord(c.main_done[b], c.sm), "record");
+    c.pending[b] = true;
   }
   return 0;
 }
@@ -486,6 +576,35 @@ int edv_verify_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uint
   return 0;
 }
 
+int edv_verify_batch_dev_pipelined(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
+                                   const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept,
+                                   int device) {
+  g_err.clear();
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((err = ctx_init(*c, device))) return err;
+  HIPOK(hipSetDevice(device), "hipSetDevice");
+  if (n == 0) return 0;
+  return launch_pipelined(*c, d_sigs, d_pks, d_msgs, d_msg_off, msg_base, n, d_accept);
+}
+
+int edv_pipeline_sync(int device) {
+  g_err.clear();
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((err = ctx_init(*c, device))) return err;
+  HIPOK(hipSetDevice(device), "hipSetDevice");
+  if (!c->pipe_ready) return 0;
+  HIPOK(hipStreamSynchronize(c->sp), "pipeline sync");
+  HIPOK(hipStreamSynchronize(c->sm), "pipeline sync");
+  c->pending[0] = c->pending[1] = false;
+  return 0;
+}
+
 int edv_time_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
                        const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, int device,
                        int iters, float* ms_out) {
@@ -577,10 +696,13 @@ int edv_set_chunk(int device, uint64_t chunk) {
   HIPOK(hipStreamSynchronize(c->stream), "stream sync");
   if (chunk == 0) chunk = kChunkDefault;
   if (chunk < kBlock || chunk > (uint64_t(1) << 24)) return set_err(EDV_E_ARG, "chunk out of range");
+  if (c->pipe_ready) {
+    HIPOK(hipStreamSynchronize(c->sp), "pipeline sync");
+    HIPOK(hipStreamSynchronize(c->sm), "pipeline sync");
+  }
   c->chunk = (chunk / kBlock) * kBlock;
-  if (c->atab.ensure(c->chunk * kAWords * 4) || c->dig.ensure(c->chunk * 16 * 4) || c->alive.ensure(c->chunk) ||
-      c->perm.ensure(c->chunk * 4))
-    return EDV_E_OOM;
+  if (c->st.ensure(c->chunk)) return EDV_E_OOM;
+  if (c->pipe_ready && (c->pst[0].ensure(c->chunk) || c->pst[1].ensure(c->chunk))) return EDV_E_OOM;
   return 0;
 }
 
@@ -602,12 +724,12 @@ int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uin
   va.off = d_msg_off;
   va.msg_base = msg_base;
   va.accept = d_accept;
-  va.st = ChunkState{static_cast<int32_t*>(c->atab.p), static_cast<uint32_t*>(c->dig.p),
-                     static_cast<uint8_t*>(c->alive.p), c->chunk, static_cast<uint32_t*>(c->perm.p)};
+  va.st = ChunkState{static_cast<int32_t*>(c->st.atab.p), static_cast<uint32_t*>(c->st.dig.p),
+                     static_cast<uint8_t*>(c->st.alive.p), c->chunk, static_cast<uint32_t*>(c->st.perm.p)};
   va.btab = c->btab;
   va.base = 0;
-  uint32_t* hist = static_cast<uint32_t*>(c->bucket_ctr.p);
-  const bool bucket = getenv("EDV_NO_BUCKET") == nullptr;
+  uint32_t* hist = static_cast<uint32_t*>(c->st.bucket_ctr.p);
+  const bool bucket = bucketing_enabled(true);
   if (!bucket) va.st.perm = nullptr;
   va.n = n;
   const unsigned blocks = unsigned((n + kBlock - 1) / kBlock);
@@ -619,7 +741,7 @@ int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uin
       HIPOK(hipMemsetAsync(hist, 0, 2 * kBuckets * 4, c->stream), "memset buckets");
       edv_bucket_hist_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(d_msg_off, 0, n, hist);
       edv_bucket_scatter_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(d_msg_off, 0, n, hist, hist + kBuckets,
-                                                                               static_cast<uint32_t*>(c->perm.p));
+                                                                               static_cast<uint32_t*>(c->st.perm.p));
     }
     HIPOK(hipEventRecord(ev[0], c->stream), "record");
     edv_prep_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(va);

@@ -60,6 +60,10 @@ def lib():
         h.edv_verify_batch.restype = ctypes.c_int
         h.edv_verify_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, vp]
         h.edv_verify_batch_dev.restype = ctypes.c_int
+        h.edv_verify_batch_dev_pipelined.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int]
+        h.edv_verify_batch_dev_pipelined.restype = ctypes.c_int
+        h.edv_pipeline_sync.argtypes = [ctypes.c_int]
+        h.edv_pipeline_sync.restype = ctypes.c_int
         h.edv_time_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_float)]
         h.edv_time_batch_dev.restype = ctypes.c_int
@@ -224,6 +228,18 @@ class DeviceBuffer:
 def verify_device(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, msg_base=0, stream=None):
     """Device-resident verify (pointers are ints); async on `stream` if given."""
     _check(lib().edv_verify_batch_dev(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, stream))
+
+
+def verify_device_pipelined(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, msg_base=0):
+    """Enqueue a device-resident batch on the library's two-stream pipeline (the
+    prep kernel of the next batch overlaps the main kernel of this one); the
+    verdicts are in d_accept after pipeline_sync(device)."""
+    _check(lib().edv_verify_batch_dev_pipelined(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device))
+
+
+def pipeline_sync(device: int = 0):
+    """Wait for every pipelined batch submitted on `device`."""
+    _check(lib().edv_pipeline_sync(device))
 
 
 def sign_device(d_seeds, d_msgs, d_off, n, d_pks, d_sigs, device=0, msg_base=0, stream=None):

@@ -81,6 +81,11 @@ class DeviceBatch:
         edv.verify_device(self.d_sigs.ptr, self.d_pks.ptr, self.d_msgs.ptr, self.d_off.ptr, self.n,
                           self.d_accept.ptr, self.device, stream=stream)
 
+    def submit(self):
+        """Pipelined verify (edv_verify_batch_dev_pipelined); results after edv.pipeline_sync."""
+        edv.verify_device_pipelined(self.d_sigs.ptr, self.d_pks.ptr, self.d_msgs.ptr, self.d_off.ptr, self.n,
+                                    self.d_accept.ptr, self.device)
+
     def accept(self):
         return self.d_accept.download(self.n)
 

@@ -182,3 +182,27 @@ def test_device_mask_selects_device():
     assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off, device_mask=1), want)
     with pytest.raises(edv.EdvUnavailable):
         edv.verify_arrays(sigs, pks, msgs, off, device_mask=1 << 20)
+
+
+def test_pipelined_submission_matches():
+    """edv_verify_batch_dev_pipelined: several different batches in flight on the
+    two-stream pipeline (state sets alternate) give each batch its own verdicts."""
+    batches = []
+    for k in range(5):
+        sigs, pks, msgs, off = orc.corpus(0x919 + k, 0, 1500 + 300 * k, mode=k % 2, invalid_permille=150)
+        want = checker(sigs, pks, msgs, off)
+        bufs = [edv.DeviceBuffer(a.nbytes + 64) for a in (sigs, pks, msgs, off)]
+        for b, a in zip(bufs, (sigs, pks, msgs, off)):
+            b.upload(a)
+        acc = edv.DeviceBuffer(len(want))
+        batches.append((bufs, acc, want))
+    try:
+        edv.set_chunk(0, 1024)  # several chunks per batch: the pipeline alternates within a batch too
+        for _ in range(2):
+            for bufs, acc, want in batches:
+                edv.verify_device_pipelined(bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, len(want), acc.ptr)
+            edv.pipeline_sync(0)
+            for bufs, acc, want in batches:
+                assert np.array_equal(acc.download(len(want)), want)
+    finally:
+        edv.set_chunk(0, 0)
