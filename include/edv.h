@@ -67,6 +67,20 @@ int edv_verify_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uint
                          int device, void *stream);
 
 /*
+ * Batch SHA-256: out[32 i .. 32 i + 32) = SHA-256 of message i
+ * (msgs/msg_off as in edv_verify_batch).  Host buffers, synchronous, sharded over
+ * device_mask like edv_verify_batch.  Replaces, per request,
+ * plenum/common/request.py:71-72 Request.getDigest (sha256 of the signing bytes,
+ * hex-encoded by the caller) and plenum/server/domain_req_handler.py:166-167
+ * nym_to_state_key (sha256 of the DID string).
+ */
+int edv_sha256_batch(const uint8_t *msgs, const uint64_t *msg_off, uint64_t n, uint8_t *out, uint32_t device_mask);
+/* Device-resident form, async on `stream` (NULL = library stream, synchronised);
+ * d_msgs readable 8 bytes past the last message byte; d_out n x 32 bytes. */
+int edv_sha256_batch_dev(const uint8_t *d_msgs, const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n,
+                         uint8_t *d_out, int device, void *stream);
+
+/*
  * Pipelined submission of device-resident batches (a continuous stream of
  * client batches, e.g. one per Node prod): enqueues the batch and returns
  * without waiting.  Consecutive submissions alternate between two internal

@@ -7,6 +7,7 @@
 #include <string.h>
 #include <vector>
 #include "edv_verify_core.h"
+#include "edv_sha256.h"
 
 using namespace edv;
 
@@ -83,6 +84,14 @@ int hc_decompress_negate(const uint8_t* in, uint8_t* out) {
   ge_p2_tobytes(o, ge_p3_to_p2(p));
   store_words(out, o, 8);
   return ok ? 0 : -1;
+}
+// SHA-256 of m at a chosen misalignment of the copy (the kernel reads aligned words)
+void hc_sha256(const uint8_t* m, uint64_t mlen, int misalign, uint8_t* out32) {
+  std::vector<uint8_t> buf(mlen + 48, 0xA5);
+  if (mlen) memcpy(buf.data() + 16 + misalign, m, mlen);
+  uint32_t o[8];
+  sha256_msg(o, buf.data() + 16 + misalign, mlen);
+  store_words(out32, o, 8);
 }
 void hc_btab(int32_t* out) { memcpy(out, btab().w.data(), sizeof(int32_t) * kBEntries * kBStride); }
 int hc_sign_batch(const uint8_t* seeds, const uint8_t* msgs, const uint64_t* off, uint64_t n, uint8_t* pks,

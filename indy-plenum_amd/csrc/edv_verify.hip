@@ -25,6 +25,7 @@
 #include <string>
 
 #include "edv_verify_core.h"
+#include "edv_sha256.h"
 #include "../../include/edv.h"
 
 using namespace edv;
@@ -264,6 +265,19 @@ __global__ __launch_bounds__(kBlock) void edv_bucket_scatter_kernel(const uint64
 __global__ void edv_btab_kernel(int32_t* out) {
   const int j = threadIdx.x + blockIdx.x * blockDim.x;
   if (j < kBEntries) btab_entry(out + j * kBStride, j);
+}
+
+// Row f-3: SHA-256 of n messages, one per lane -> 32-byte digests (out: n x 8 words).
+__global__ __launch_bounds__(kBlock) void edv_sha256_kernel(const uint8_t* msgs, const uint64_t* off, uint64_t msg_base,
+                                                            uint64_t n, uint32_t* out) {
+  const uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t o0 = off[i] - msg_base, o1 = off[i + 1] - msg_base;
+  uint32_t d[8];
+  sha256_msg(d, msgs + o0, o1 - o0);
+  uint4* po = reinterpret_cast<uint4*>(out + 8 * i);
+  po[0] = make_uint4(d[0], d[1], d[2], d[3]);
+  po[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
 // ------------------------------------------------------------ host runtime
@@ -513,6 +527,67 @@ int run_shard(int dev, const uint8_t* sigs, const uint8_t* pks, const uint8_t* m
   return 0;
 }
 
+int launch_sha256(const uint8_t* d_msgs, const uint64_t* d_off, uint64_t msg_base, uint64_t n, uint8_t* d_out,
+                  hipStream_t s) {
+  if (n == 0) return 0;
+  const unsigned blocks = unsigned((n + kBlock - 1) / kBlock);
+  edv_sha256_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_msgs, d_off, msg_base, n, reinterpret_cast<uint32_t*>(d_out));
+  HIPOK(hipGetLastError(), "sha256 launch");
+  return 0;
+}
+
+// SHA-256 digests of messages [lo, hi) on one device, host buffers
+int run_digest_shard(int dev, const uint8_t* msgs, const uint64_t* off, uint64_t lo, uint64_t hi, uint8_t* out) {
+  int err = 0;
+  DevCtx* c = get_ctx(dev, &err);
+  if (!c) return err;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((err = ctx_init(*c, dev))) return err;
+  HIPOK(hipSetDevice(dev), "hipSetDevice");
+  const uint64_t n = hi - lo;
+  if (n == 0) return 0;
+  const uint64_t mbase = off[lo], mbytes = off[hi] - off[lo];
+  if (c->msgs.ensure(mbytes + 64) || c->off.ensure((n + 1) * 8) || c->sigs.ensure(n * 32)) return EDV_E_OOM;
+  if (mbytes) HIPOK(hipMemcpyAsync(c->msgs.p, msgs + mbase, mbytes, hipMemcpyHostToDevice, c->stream), "h2d msgs");
+  HIPOK(hipMemcpyAsync(c->off.p, off + lo, (n + 1) * 8, hipMemcpyHostToDevice, c->stream), "h2d off");
+  if ((err = launch_sha256(static_cast<uint8_t*>(c->msgs.p), static_cast<uint64_t*>(c->off.p), mbase, n,
+                           static_cast<uint8_t*>(c->sigs.p), c->stream)))
+    return err;
+  HIPOK(hipMemcpyAsync(out + 32 * lo, c->sigs.p, n * 32, hipMemcpyDeviceToHost, c->stream), "d2h digests");
+  HIPOK(hipStreamSynchronize(c->stream), "stream sync");
+  return 0;
+}
+
+// Validate a host batch and split [0, n) over the devices of device_mask, one
+// host thread per device; shard(dev, lo, hi) does the work.
+template <class Shard>
+int for_each_shard(uint64_t n, uint32_t device_mask, Shard shard) {
+  int ndev;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    ndev = device_count_locked();
+  }
+  std::vector<int> devs;
+  for (int d = 0; d < ndev && d < 32; d++)
+    if (device_mask == 0 || (device_mask >> d) & 1u) devs.push_back(d);
+  if (devs.empty()) return set_err(EDV_E_NODEV, "no device selected / visible");
+  const uint64_t g = devs.size();
+  if (g == 1) return shard(devs[0], uint64_t(0), n);
+  std::vector<int> rc(g, 0);
+  std::vector<std::string> errs(g);
+  std::vector<std::thread> th;
+  for (uint64_t k = 0; k < g; k++) {
+    th.emplace_back([&, k]() {
+      rc[k] = shard(devs[k], n * k / g, n * (k + 1) / g);
+      errs[k] = g_err;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (uint64_t k = 0; k < g; k++)
+    if (rc[k]) { g_err = errs[k]; return rc[k]; }
+  return 0;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ C-ABI
@@ -534,29 +609,35 @@ int edv_verify_batch(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msg
   if (!msgs && msg_off[n] != msg_off[0]) return set_err(EDV_E_ARG, "null msgs");
   for (uint64_t i = 0; i < n; i++)
     if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_E_ARG, "msg_off not non-decreasing");
-  int ndev;
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    ndev = device_count_locked();
-  }
-  std::vector<int> devs;
-  for (int d = 0; d < ndev && d < 32; d++)
-    if (device_mask == 0 || (device_mask >> d) & 1u) devs.push_back(d);
-  if (devs.empty()) return set_err(EDV_E_NODEV, "no device selected / visible");
-  const uint64_t g = devs.size();
-  if (g == 1) return run_shard(devs[0], sigs, pks, msgs, msg_off, 0, n, accept);
-  std::vector<int> rc(g, 0);
-  std::vector<std::string> errs(g);
-  std::vector<std::thread> th;
-  for (uint64_t k = 0; k < g; k++) {
-    th.emplace_back([&, k]() {
-      rc[k] = run_shard(devs[k], sigs, pks, msgs, msg_off, n * k / g, n * (k + 1) / g, accept);
-      errs[k] = g_err;
-    });
-  }
-  for (auto& t : th) t.join();
-  for (uint64_t k = 0; k < g; k++)
-    if (rc[k]) { g_err = errs[k]; return rc[k]; }
+  return for_each_shard(n, device_mask, [&](int dev, uint64_t lo, uint64_t hi) {
+    return run_shard(dev, sigs, pks, msgs, msg_off, lo, hi, accept);
+  });
+}
+
+int edv_sha256_batch(const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, uint8_t* out, uint32_t device_mask) {
+  g_err.clear();
+  if (n == 0) return 0;
+  if (!msg_off || !out) return set_err(EDV_E_ARG, "null pointer");
+  if (!msgs && msg_off[n] != msg_off[0]) return set_err(EDV_E_ARG, "null msgs");
+  for (uint64_t i = 0; i < n; i++)
+    if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_E_ARG, "msg_off not non-decreasing");
+  return for_each_shard(n, device_mask, [&](int dev, uint64_t lo, uint64_t hi) {
+    return run_digest_shard(dev, msgs, msg_off, lo, hi, out);
+  });
+}
+
+int edv_sha256_batch_dev(const uint8_t* d_msgs, const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n,
+                         uint8_t* d_out, int device, void* stream) {
+  g_err.clear();
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((err = ctx_init(*c, device))) return err;
+  HIPOK(hipSetDevice(device), "hipSetDevice");
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  if ((err = launch_sha256(d_msgs, d_msg_off, msg_base, n, d_out, s))) return err;
+  if (!stream) HIPOK(hipStreamSynchronize(s), "stream sync");
   return 0;
 }
 

@@ -60,6 +60,10 @@ def lib():
         h.edv_verify_batch.restype = ctypes.c_int
         h.edv_verify_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, vp]
         h.edv_verify_batch_dev.restype = ctypes.c_int
+        h.edv_sha256_batch.argtypes = [vp, vp, u64, vp, ctypes.c_uint32]
+        h.edv_sha256_batch.restype = ctypes.c_int
+        h.edv_sha256_batch_dev.argtypes = [vp, vp, u64, u64, vp, ctypes.c_int, vp]
+        h.edv_sha256_batch_dev.restype = ctypes.c_int
         h.edv_verify_batch_dev_pipelined.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int]
         h.edv_verify_batch_dev_pipelined.restype = ctypes.c_int
         h.edv_pipeline_sync.argtypes = [ctypes.c_int]
@@ -146,6 +150,37 @@ def verify_arrays(sigs, pks, msgs, offsets, device_mask: int = 0) -> np.ndarray:
     _check(lib().edv_verify_batch(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, off.ctypes.data, n,
                                   accept.ctypes.data, device_mask))
     return accept
+
+
+def sha256_arrays(msgs, offsets, device_mask: int = 0) -> np.ndarray:
+    """SHA-256 of n messages in the C-ABI layout -> (n, 32) uint8 digests (row f-3)."""
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(off) - 1
+    if n <= 0:
+        return np.zeros((0, 32), dtype=np.uint8)
+    if not isinstance(msgs, np.ndarray):
+        msgs = np.frombuffer(bytes(msgs) or b"\0", dtype=np.uint8)
+    if int(off[-1]) > msgs.nbytes:
+        raise ValueError("offsets exceed the message buffer")
+    out = np.zeros((n, 32), dtype=np.uint8)
+    _check(lib().edv_sha256_batch(msgs.ctypes.data, off.ctypes.data, n, out.ctypes.data, device_mask))
+    return out
+
+
+def sha256_batch(messages, device_mask: int = 0):
+    """list[bytes] -> list[32-byte digest] (hashlib.sha256(m).digest() for each m)."""
+    messages = list(messages)
+    if not messages:
+        return []
+    off = np.zeros(len(messages) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(m) for m in messages])
+    d = sha256_arrays(b"".join(messages), off, device_mask)
+    return [bytes(r) for r in d]
+
+
+def sha256_device(d_msgs, d_off, n, d_out, device=0, msg_base=0, stream=None):
+    """Device-resident batch SHA-256: d_out gets n x 32 bytes."""
+    _check(lib().edv_sha256_batch_dev(d_msgs, d_off, msg_base, n, d_out, device, stream))
 
 
 def verify_detached_batch(items, device_mask: int = 0):

@@ -46,3 +46,9 @@ def pack_batch(recs):
     off = np.zeros(len(recs) + 1, dtype=np.uint64)
     off[1:] = np.cumsum([len(r[4]) for r in recs])
     return sigs, pks, msgs, off
+
+
+def load_serializer_golden():
+    """Reference SigningSerializer outputs: [{"msg", "ignore", "ser"}] (make_serializer_golden.py)."""
+    with open(os.path.join(GOLDEN, "serializer_golden.json")) as f:
+        return json.load(f)["cases"]

@@ -1,5 +1,5 @@
 """ctypes access to libedv_hostcheck.so: the KERNEL's own math and per-signature
-algorithm (indy-plenum_amd/csrc/edv_math.h, edv_verify_core.h) compiled for the
+algorithm (indy-plenum_amd/csrc/edv_math.h, edv_verify_core.h, edv_sha256.h) compiled for the
 CPU.  Test harness only."""
 import ctypes
 import os
@@ -14,10 +14,11 @@ _lib = None
 def load():
     global _lib
     if _lib is None:
-        srcs = [os.path.join(CSRC, f) for f in ("edv_hostcheck.cpp", "edv_math.h", "edv_verify_core.h")]
+        srcs = [os.path.join(CSRC, f) for f in ("edv_hostcheck.cpp", "edv_math.h", "edv_verify_core.h", "edv_sha256.h")]
         if not os.path.exists(SO) or os.path.getmtime(SO) < max(os.path.getmtime(s) for s in srcs):
             subprocess.check_call(["make", "-s", "-C", CSRC, "../libedv_hostcheck.so"])
         _lib = ctypes.CDLL(SO)
         _lib.hc_hram.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
+        _lib.hc_sha256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
         _lib.hc_verify_batch.argtypes = [ctypes.c_char_p] * 3 + [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
     return _lib

@@ -70,3 +70,20 @@ def test_signing_serializer_rules():
     assert serialize_msg_for_signing({'a': {'b': 1, 'c': 2}}, topLevelKeysToIgnore=['b']) == b'a:b:1|c:2'
     with pytest.raises(Exception):
         serialize_msg_for_signing({'a': (1, 2)})  # tuples are not acceptable types
+
+
+def test_signing_state_matches_request_semantics():
+    """digest.signing_state restates Request.signingState (request.py:77-87) and
+    Request.identifier (request.py:110-112, 124-126) for request dicts."""
+    from indy_plenum_amd import digest
+    req = {"identifier": "L5AD5g65TDQr1PPHHRoiGf", "reqId": 1513945121191691, "protocolVersion": 1,
+           "operation": {"dest": "GEzcdDLhCpGCYRHW82kjHd", "type": "1"}, "signature": "xyz"}
+    assert digest.signing_state(req) == {"identifier": "L5AD5g65TDQr1PPHHRoiGf", "reqId": 1513945121191691,
+                                         "operation": {"dest": "GEzcdDLhCpGCYRHW82kjHd", "type": "1"},
+                                         "protocolVersion": 1}
+    multi = {"reqId": 5, "operation": {"type": "1"}, "signatures": {"b": "s1", "a": "s2"}}
+    assert digest.signing_state(multi) == {"identifier": "a,b", "reqId": 5, "operation": {"type": "1"}}
+    assert digest.signing_state(multi, identifier="z")["identifier"] == "z"
+    import pytest
+    with pytest.raises(AttributeError):
+        digest.signing_state({"reqId": 1, "operation": {}})

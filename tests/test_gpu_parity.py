@@ -206,3 +206,43 @@ def test_pipelined_submission_matches():
                 assert np.array_equal(acc.download(len(want)), want)
     finally:
         edv.set_chunk(0, 0)
+
+
+def test_sha256_batch_vs_hashlib():
+    """Row f-3: edv_sha256_batch (gfx950) == hashlib.sha256 for every message of a
+    ragged batch (empty, block-boundary and 4 KB lengths, unaligned starts), on
+    the host path and the device-resident path."""
+    import random
+    r = random.Random(12)
+    lens = list(range(0, 140)) + [r.randrange(0, 4097) for _ in range(3000)] + [4096, 55, 56, 64]
+    msgs = [bytes(r.getrandbits(8) for _ in range(n)) for n in lens]
+    got = edv.sha256_batch(msgs)
+    assert got == [hashlib.sha256(m).digest() for m in msgs]
+    assert edv.sha256_batch([]) == []
+    # device-resident, with a msg_base and a leading pad so starts are unaligned
+    blob = b"\x11" * 3 + b"".join(msgs) + b"\0" * 16
+    off = np.zeros(len(msgs) + 1, dtype=np.uint64)
+    off[0] = 3
+    off[1:] = 3 + np.cumsum(lens)
+    dm, do, dd = edv.DeviceBuffer(len(blob)), edv.DeviceBuffer(off.nbytes), edv.DeviceBuffer(32 * len(msgs))
+    dm.upload(np.frombuffer(blob, np.uint8))
+    do.upload(off)
+    edv.sha256_device(dm.ptr, do.ptr, len(msgs), dd.ptr)
+    assert dd.download(32 * len(msgs)).tobytes() == b"".join(hashlib.sha256(m).digest() for m in msgs)
+
+
+def test_request_digests_and_state_keys():
+    """Request.getDigest / nym_to_state_key semantics (request.py:71-72,
+    domain_req_handler.py:166-167), pinned by the reference serializer's own
+    outputs: for golden requests whose keys are exactly signingState's, the
+    digest must be the hex SHA-256 of the reference's serialized bytes."""
+    from indy_plenum_amd import digest
+    keys = {"identifier", "reqId", "operation", "protocolVersion"}
+    cases = [c for c in golden_io.load_serializer_golden() if isinstance(c["msg"], dict) and not c["ignore"]
+             and {"identifier", "reqId", "operation"} <= set(c["msg"]) <= keys]
+    assert len(cases) >= 3
+    reqs = [dict(c["msg"], signature="sig-is-not-hashed") for c in cases]
+    want = [hashlib.sha256(c["ser"].encode()).hexdigest() for c in cases]
+    assert digest.request_digests(reqs) == want
+    nyms = [c["msg"]["identifier"] for c in cases] + ["", "V4SGRU86Z58d6TV7PBUe6f"]
+    assert digest.nym_state_keys(nyms) == [hashlib.sha256(n.encode()).digest() for n in nyms]

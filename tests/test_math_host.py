@@ -108,6 +108,19 @@ def test_hram_sha512_all_lengths():
         assert d.raw == hashlib.sha512(R + A + m).digest(), n
 
 
+def test_sha256_all_lengths_and_alignments():
+    """The kernel's SHA-256 (row f-3) vs hashlib: every length across the 1-, 2-
+    and 3-block padding boundaries, long messages, and all 4 misalignments."""
+    hc = hostcheck_lib.load()
+    r = random.Random(10)
+    d = ctypes.create_string_buffer(32)
+    for n in list(range(0, 200)) + [247, 255, 256, 1000, 4095, 4096, 4097]:
+        m = bytes(r.getrandbits(8) for _ in range(n))
+        for mis in range(4):
+            hc.hc_sha256(m, len(m), mis, d)
+            assert d.raw == hashlib.sha256(m).digest(), (n, mis)
+
+
 def test_kernel_algorithm_on_cpu_matches_libsodium_golden(golden, golden_meta):
     hc = hostcheck_lib.load()
     sigs, pks, msgs, off = golden_io.pack_batch(golden)
