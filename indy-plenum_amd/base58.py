@@ -31,7 +31,29 @@ def b58encode_int(i, default_one=True):
     return string
 
 
+try:  # native fast path (csrc/edv_host.cpp, row f-1); NotImplemented -> the restatement below
+    from . import _edvhost as _native
+except ImportError:  # pragma: no cover - the in-tree build always provides it
+    _native = None
+
+
 def b58encode(v):
+    if _native is not None:
+        r = _native.b58encode(v)
+        if r is not NotImplemented:
+            return r
+    return _b58encode_py(v)
+
+
+def b58decode(v):
+    if _native is not None:
+        r = _native.b58decode(v)
+        if r is not NotImplemented:
+            return r
+    return _b58decode_py(v)
+
+
+def _b58encode_py(v):
     v = scrub_input(v)
     n_pad = len(v)
     v = v.lstrip(b'\0')
@@ -52,7 +74,7 @@ def b58decode_int(v):
     return decimal
 
 
-def b58decode(v):
+def _b58decode_py(v):
     v = v.rstrip()
     v = scrub_input(v)
     origlen = len(v)

@@ -18,6 +18,8 @@ import threading
 
 import numpy as np
 
+from . import _edvhost  # native host-side packing (csrc/edv_host.cpp, row f-1)
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("EDV_LIB", os.path.join(_HERE, "libedv.so"))
 
@@ -206,24 +208,16 @@ def open_batch(items, device_mask: int = 0):
     signature of any length is accepted iff (sm[:64], sm[64:]) verifies; sm
     shorter than 64 bytes rejects without reaching the GPU.  pk must be 32 bytes.
     """
-    items = list(items)
+    items = [(bytes(s), bytes(m), bytes(p)) for s, m, p in items]
     out = [False] * len(items)
-    todo = []
-    idx = []
-    for k, (sig, msg, pk) in enumerate(items):
-        if len(pk) != 32:
-            raise ValueError("public key must be 32 bytes")
-        if len(sig) == 64:
-            todo.append((sig, msg, pk))
-        else:
-            sm = bytes(sig) + bytes(msg)
-            if len(sm) < 64:
-                continue
-            todo.append((sm[:64], sm[64:], pk))
-        idx.append(k)
-    if todo:
-        for k, ok in zip(idx, verify_detached_batch(todo, device_mask)):
-            out[k] = ok
+    if not items:
+        return out
+    sigs, pks, msgs, off, idx = _edvhost.pack_open_batch(items)
+    if idx:
+        acc = verify_arrays(np.frombuffer(sigs, np.uint8), np.frombuffer(pks, np.uint8),
+                            np.frombuffer(msgs, np.uint8), np.frombuffer(off, np.uint64), device_mask)
+        for k, ok in zip(idx, acc):
+            out[k] = bool(ok)
     return out
 
 

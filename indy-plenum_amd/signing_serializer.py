@@ -48,6 +48,15 @@ class SigningSerializer:
 
 signing_serializer = SigningSerializer()
 
+try:  # native fast path (csrc/edv_host.cpp, row f-1); NotImplemented -> the class above
+    from . import _edvhost as _native
+except ImportError:  # pragma: no cover - the in-tree build always provides it
+    _native = None
+
 
 def serialize_msg_for_signing(msg, topLevelKeysToIgnore=None):
+    if _native is not None:
+        r = _native.serialize(msg, topLevelKeysToIgnore)
+        if r is not NotImplemented:
+            return r
     return signing_serializer.serialize(msg, topLevelKeysToIgnore=topLevelKeysToIgnore)

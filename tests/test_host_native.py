@@ -1,0 +1,129 @@
+"""Row f-1: the native host prep (_edvhost, csrc/edv_host.cpp) gives exactly the
+results of the Python restatements of base58 1.0.0 and SigningSerializer (which
+are pinned by the reference's fixtures and outputs in test_base58_serializer.py),
+on fixed edge cases and on randomized inputs; anything it does not handle falls
+back (NotImplemented) so the reference's exceptions are unchanged."""
+import random
+
+import numpy as np
+import pytest
+
+from indy_plenum_amd import _edvhost, base58, edv, signing_serializer
+from indy_plenum_amd.signing_serializer import SigningSerializer, serialize_msg_for_signing
+
+
+def test_native_module_is_loaded():
+    assert base58._native is _edvhost and signing_serializer._native is _edvhost
+
+
+def py_dec(v):
+    try:
+        return base58._b58decode_py(v)
+    except Exception as ex:
+        return type(ex)
+
+
+def api_dec(v):
+    try:
+        return base58.b58decode(v)
+    except Exception as ex:
+        return type(ex)
+
+
+def test_b58_edge_cases():
+    cases = ["", "1", "11", "111z", "2", "z", "zz", " 1A ", "1A\n", "1A\x1c", "1A\t\r\x0b\x0c", "0", "O", "I",
+             "l", "abc!", "é", "1é", "　", "A　", b"", b"1", b"1A \n", b"1A\x1c", b"\x00", b"zz",
+             "V4SGRU86Z58d6TV7PBUe6f", "5rArie7XKukPCaEwq5XGQJnM9Fc5aZE3M9HAPVfMU2xC", 42, None, bytearray(b"1A")]
+    for c in cases:
+        assert api_dec(c) == py_dec(c), repr(c)
+        nat = _edvhost.b58decode(c)
+        if nat is not NotImplemented:
+            assert nat == py_dec(c), repr(c)
+
+
+def test_b58_random_roundtrip():
+    r = random.Random(3)
+    for _ in range(3000):
+        raw = bytes([0] * r.randrange(4)) + bytes(r.getrandbits(8) for _ in range(r.randrange(0, 70)))
+        enc = base58.b58encode(raw)
+        assert enc == base58._b58encode_py(raw)
+        assert base58.b58decode(enc) == raw == base58._b58decode_py(enc)
+        s = enc.decode() + r.choice(["", " ", "\n", "  \t"])
+        assert base58.b58decode(s) == base58._b58decode_py(s)
+        t = "".join(r.choice("123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz0OIl!")
+                    for _ in range(r.randrange(0, 50)))
+        assert api_dec(t) == py_dec(t)
+
+
+def _rand_obj(r, depth=0):
+    k = r.randrange(9 if depth < 3 else 6)
+    if k == 0:
+        return r.choice(["", "a", "x|y:z", "ünï", "日本", "1,2"])
+    if k == 1:
+        return r.choice([0, 1, -7, 2**70, -(2**64), 10**20])
+    if k == 2:
+        return r.choice([0.1, 1.5, -2.0, 1e300, 1e-7, float("inf")])
+    if k == 3:
+        return r.choice([True, False])
+    if k == 4:
+        return None
+    if k == 5:
+        return r.choice(["NYM", "1", "~abc"])
+    if k == 6:
+        return [_rand_obj(r, depth + 1) for _ in range(r.randrange(4))]
+    return {r.choice(["a", "b", "B", "type", "dest", "verkey", "é", "_", "10", "9", "zz"]) + str(i):
+            _rand_obj(r, depth + 1) for i in range(r.randrange(5))}
+
+
+def test_serializer_native_equals_restatement():
+    r = random.Random(4)
+    ss = SigningSerializer()
+    for _ in range(4000):
+        obj = {"identifier": "L5AD5g65TDQr1PPHHRoiGf", "operation": _rand_obj(r), "reqId": r.randrange(10**16),
+               "extra": _rand_obj(r)}
+        for ignore in (None, ["extra"], ("reqId", "extra"), {"operation"}):
+            want = ss.serialize(obj, topLevelKeysToIgnore=ignore)
+            assert _edvhost.serialize(obj, ignore) == want
+            assert serialize_msg_for_signing(obj, topLevelKeysToIgnore=ignore) == want
+
+
+def test_serializer_fallbacks_keep_reference_errors():
+    ss = SigningSerializer()
+    for bad in ({"a": (1, 2)}, {"a": {1: "x"}}, {"a": b"bytes"}, {"a": object()}, {1: "x", 2: "y"}):
+        assert _edvhost.serialize(bad, None) is NotImplemented
+        try:
+            want = ss.serialize(bad)
+        except Exception as ex:
+            with pytest.raises(type(ex)):
+                serialize_msg_for_signing(bad)
+        else:
+            assert serialize_msg_for_signing(bad) == want
+    s = {"a": "\ud800"}  # lone surrogate: UnicodeEncodeError from the restatement
+    assert _edvhost.serialize(s, None) is NotImplemented
+    with pytest.raises(UnicodeEncodeError):
+        serialize_msg_for_signing(s)
+
+
+def test_pack_open_batch_positional_split():
+    r = random.Random(5)
+    items = []
+    for _ in range(500):
+        ls = r.choice([0, 10, 63, 64, 65, 100])
+        lm = r.choice([0, 1, 20, 300])
+        items.append((bytes(r.getrandbits(8) for _ in range(ls)), bytes(r.getrandbits(8) for _ in range(lm)),
+                      bytes(r.getrandbits(8) for _ in range(32))))
+    sigs, pks, msgs, off, idx = _edvhost.pack_open_batch(items)
+    off = np.frombuffer(off, np.uint64)
+    want_idx = [k for k, (s, m, _p) in enumerate(items) if len(s) + len(m) >= 64]
+    assert idx == want_idx and len(off) == len(idx) + 1
+    for j, k in enumerate(idx):
+        s, m, p = items[k]
+        sm = s + m
+        assert sigs[64 * j:64 * j + 64] == sm[:64]
+        assert msgs[off[j]:off[j + 1]] == sm[64:]
+        assert pks[32 * j:32 * j + 32] == p
+    assert len(msgs) >= off[-1] + 16
+    with pytest.raises(ValueError):
+        _edvhost.pack_open_batch([(b"x" * 64, b"", b"k" * 31)])
+    with pytest.raises(ValueError):
+        edv.open_batch([(b"x" * 64, b"", b"k" * 31)])
