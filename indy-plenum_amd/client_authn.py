@@ -25,6 +25,11 @@ from typing import Dict
 
 from . import base58
 from . import edv
+
+try:  # native host prep (csrc/edv_host.cpp, row f-1)
+    from . import _edvhost
+except ImportError:  # pragma: no cover - the in-tree build always provides it
+    _edvhost = None
 from .constants import (ACTION_TYPES, FEES, IDENTIFIER, QUERY_TYPES, ROLE, SIGNATURE, SIGNATURES, VERKEY,
                         WRITE_TYPES)
 from .exceptions import (CouldNotAuthenticate, EmptyIdentifier, EmptySignature, InsufficientCorrectSignatures,
@@ -150,9 +155,12 @@ class NaclAuthNr(ClientAuthNr):
         reference's authenticate_multi would have raised (re-raised directly
         when raise_single is set and there is one call)."""
         jobs = []
-        plans = []
-        for msg, signatures, threshold, verifier in calls:
-            plans.append(self._plan_multi(msg, signatures, threshold, verifier or DidVerifier, jobs))
+        plans = [self._plan_multi(msg, signatures, threshold, verifier or DidVerifier, jobs)
+                 for msg, signatures, threshold, verifier in calls]
+        return self._run_plans(plans, jobs, raise_single)
+
+    def _run_plans(self, plans, jobs, raise_single=False):
+        """Phase 2 (one device call for every job) and phase 3 (replay)."""
         verdicts = edv.open_batch(jobs) if jobs else []
         out = []
         for plan in plans:
@@ -273,20 +281,55 @@ class CoreAuthMixin:
     def authenticate_batch(self, reqs, verifier: Verifier = DidVerifier):
         """Batch form of authenticate over a list of request dicts: one GPU
         call for all of them.  Returns, per request, the identifier list or
-        the exception instance authenticate() would raise."""
+        the exception instance authenticate() would raise.
+
+        Requests on the common path (one signature, identifier present, verkey
+        in the in-memory `clients` map, DidVerifier giving a 32-byte key) are
+        prepared natively in one call (_edvhost.prep_core_batch, row f-1); every
+        other request goes through the Python plan, which raises exactly what
+        the reference raises."""
         out = [None] * len(reqs)
-        calls, where = [], []
+        fast = self._native_prep(reqs, verifier)
+        jobs, plans, where = [], [], []
         for k, req in enumerate(reqs):
+            pre = fast[k] if fast is not None else None
+            if pre is not None:
+                idr, sig, ser, pk = pre
+                # threshold None -> 1 signature; replay gives [idr] or InsufficientCorrectSignatures(0, 1)
+                plans.append(_Plan(1, [(idr, None, sig, ser, len(jobs))]))
+                jobs.append((sig, ser, pk))
+                where.append(k)
+                continue
             try:
                 to_serialize, signatures = self._prepare(req)
             except Exception as ex:
                 out[k] = ex
                 continue
-            calls.append((to_serialize, signatures, None, verifier))
+            plans.append(self._plan_multi(to_serialize, signatures, None, verifier or DidVerifier, jobs))
             where.append(k)
-        for k, res in zip(where, self.authenticate_multi_batch(calls)):
+        for k, res in zip(where, self._run_plans(plans, jobs)):
             out[k] = res
         return out
+
+    def _native_prep(self, reqs, verifier):
+        """_edvhost.prep_core_batch when this authenticator and verifier are the
+        stock ones (an override of any step it restates keeps the Python path)."""
+        cls = type(self)
+        if (_edvhost is None or verifier is not DidVerifier or not isinstance(getattr(self, "clients", None), dict)
+                or cls._prepare is not CoreAuthMixin._prepare
+                or cls.serializeForSig is not CoreAuthMixin.serializeForSig
+                or cls._plan_multi is not NaclAuthNr._plan_multi
+                or cls.getVerkey is not SimpleAuthNr.getVerkey
+                or base58._native is None):
+            return None
+        return _edvhost.prep_core_batch(reqs, self.clients, self.excluded_from_signing)
+
+    # requests are only read, never mutated, by the stock batch path above
+    def batch_reads_only(self):
+        cls = type(self)
+        return (cls.authenticate_batch is CoreAuthMixin.authenticate_batch
+                and cls.serializeForSig is CoreAuthMixin.serializeForSig
+                and cls._prepare is CoreAuthMixin._prepare)
 
     def serializeForSig(self, msg, identifier=None, topLevelKeysToIgnore=None):
         if not msg.get(IDENTIFIER):

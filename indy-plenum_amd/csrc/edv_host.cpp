@@ -176,6 +176,7 @@ int ser(PyObject* obj, int level, PyObject* ignore, std::string& out) {
       Py_ssize_t n;
       const char* u = PyUnicode_AsUTF8AndSize(k, &n);
       if (!u) { PyErr_Clear(); r = 0; break; }
+      Py_INCREF(v);  // str() of a value may run Python code: hold the values
       items.emplace_back(std::string(u, size_t(n)), v);
     }
     if (r == 1) {
@@ -191,6 +192,7 @@ int ser(PyObject* obj, int level, PyObject* ignore, std::string& out) {
         r = ser(items[i].second, level + 1, nullptr, out);
       }
     }
+    for (auto& it : items) Py_DECREF(it.second);
   } else if (PyList_Check(obj)) {
     const Py_ssize_t n = PyList_GET_SIZE(obj);
     for (Py_ssize_t i = 0; r == 1 && i < n; i++) {
@@ -300,7 +302,87 @@ fail:
   return nullptr;
 }
 
+// ------------------------------------------------------ CoreAuthNr fast path
+// prep_core_batch(reqs, clients, excluded) -> list, one entry per request:
+// (identifier, sig, ser, pk) when the request takes the common single-signature
+// path of CoreAuthMixin.authenticate (plenum/server/client_authn.py:211-246) ->
+// NaclAuthNr.authenticate_multi (:83-113) with SimpleAuthNr.getVerkey's
+// in-memory `clients` map (:148-160) and DidVerifier (plenum/common/verifier.py:
+// 26-52) yielding a 32-byte key; None otherwise (the Python plan handles that
+// request, including every exception the reference would raise).
+//   sig = b58decode(req["signature"])
+//   ser = SigningSerializer bytes of req minus `excluded` (identifier present)
+//   pk  = b58decode(idr) + b58decode(verkey[1:])  for a '~' abbreviated verkey
+//         b58decode(verkey)                       otherwise
+//         b58decode(idr)                          cryptonym: 32-byte idr, no verkey
+bool b58_decode_obj(PyObject* o, std::string* out) {
+  const uint8_t* p;
+  Py_ssize_t n;
+  bool is_str;
+  return PyUnicode_CheckExact(o) && text_arg(o, &p, &n, &is_str) && b58_decode(p, size_t(n), is_str, out);
+}
+
+PyObject* prep_one_core(PyObject* req, PyObject* clients, PyObject* excluded) {
+  if (!PyDict_CheckExact(req)) Py_RETURN_NONE;
+  PyObject* idr = PyDict_GetItemString(req, "identifier");
+  PyObject* sig = PyDict_GetItemString(req, "signature");
+  if (!idr || !sig || !PyUnicode_CheckExact(idr) || !PyUnicode_CheckExact(sig) || PyUnicode_GET_LENGTH(idr) == 0 ||
+      PyUnicode_GET_LENGTH(sig) == 0)
+    Py_RETURN_NONE;
+  std::string sigb, rawidr, pk;
+  if (!b58_decode_obj(sig, &sigb)) Py_RETURN_NONE;
+  PyObject* nym = PyDict_GetItemWithError(clients, idr);
+  if (!nym) {
+    if (PyErr_Occurred()) return nullptr;
+    Py_RETURN_NONE;
+  }
+  if (!PyDict_CheckExact(nym) || PyDict_GET_SIZE(nym) == 0) Py_RETURN_NONE;
+  PyObject* verkey = PyDict_GetItemString(nym, "verkey");
+  if (!verkey || !PyUnicode_CheckExact(verkey)) Py_RETURN_NONE;
+  if (!b58_decode_obj(idr, &rawidr)) Py_RETURN_NONE;
+  const Py_ssize_t vl = PyUnicode_GET_LENGTH(verkey);
+  if (vl == 0) {
+    if (rawidr.size() != 32) Py_RETURN_NONE;  // ValueError / InvalidKey paths stay in Python
+    pk = rawidr;                              // cryptonym
+  } else if (PyUnicode_READ_CHAR(verkey, 0) == '~') {
+    PyObject* abbr = PyUnicode_Substring(verkey, 1, vl);
+    if (!abbr) return nullptr;
+    std::string tail;
+    const bool ok = b58_decode_obj(abbr, &tail);
+    Py_DECREF(abbr);
+    if (!ok) Py_RETURN_NONE;
+    pk = rawidr + tail;  // b58decode(b58encode(x)) == x
+  } else if (!b58_decode_obj(verkey, &pk)) {
+    Py_RETURN_NONE;
+  }
+  if (pk.size() != 32) Py_RETURN_NONE;  // hex-encoded / empty keys: Python path
+  std::string ser_out;
+  const int r = ser(req, 0, excluded, ser_out);
+  if (r < 0) return nullptr;
+  if (r == 0) Py_RETURN_NONE;
+  return Py_BuildValue("(Oy#y#y#)", idr, sigb.data(), Py_ssize_t(sigb.size()), ser_out.data(),
+                       Py_ssize_t(ser_out.size()), pk.data(), Py_ssize_t(32));
+}
+
+PyObject* py_prep_core_batch(PyObject*, PyObject* args) {
+  PyObject *reqs, *clients, *excluded;
+  if (!PyArg_ParseTuple(args, "OO!O", &reqs, &PyDict_Type, &clients, &excluded)) return nullptr;
+  PyObject* seq = PySequence_Fast(reqs, "prep_core_batch needs a sequence of requests");
+  if (!seq) return nullptr;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  PyObject* out = PyList_New(n);
+  if (!out) { Py_DECREF(seq); return nullptr; }
+  for (Py_ssize_t k = 0; k < n; k++) {
+    PyObject* e = prep_one_core(PySequence_Fast_GET_ITEM(seq, k), clients, excluded);
+    if (!e) { Py_DECREF(out); Py_DECREF(seq); return nullptr; }
+    PyList_SET_ITEM(out, k, e);
+  }
+  Py_DECREF(seq);
+  return out;
+}
+
 PyMethodDef kMethods[] = {
+    {"prep_core_batch", py_prep_core_batch, METH_VARARGS, "CoreAuthNr single-signature fast path (None = Python)"},
     {"b58decode", py_b58decode, METH_O, "base58 1.0.0 b58decode fast path (NotImplemented = use Python)"},
     {"b58encode", py_b58encode, METH_O, "base58 1.0.0 b58encode fast path (NotImplemented = use Python)"},
     {"serialize", py_serialize, METH_VARARGS, "SigningSerializer.serialize fast path (NotImplemented = use Python)"},

@@ -208,11 +208,15 @@ def open_batch(items, device_mask: int = 0):
     signature of any length is accepted iff (sm[:64], sm[64:]) verifies; sm
     shorter than 64 bytes rejects without reaching the GPU.  pk must be 32 bytes.
     """
-    items = [(bytes(s), bytes(m), bytes(p)) for s, m, p in items]
+    items = list(items)
     out = [False] * len(items)
     if not items:
         return out
-    sigs, pks, msgs, off, idx = _edvhost.pack_open_batch(items)
+    try:
+        sigs, pks, msgs, off, idx = _edvhost.pack_open_batch(items)
+    except TypeError:  # bytearray / memoryview / list items: normalise, then pack
+        items = [(bytes(s), bytes(m), bytes(p)) for s, m, p in items]
+        sigs, pks, msgs, off, idx = _edvhost.pack_open_batch(items)
     if idx:
         acc = verify_arrays(np.frombuffer(sigs, np.uint8), np.frombuffer(pks, np.uint8),
                             np.frombuffer(msgs, np.uint8), np.frombuffer(off, np.uint64), device_mask)

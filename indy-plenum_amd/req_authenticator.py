@@ -70,7 +70,11 @@ class ReqAuthenticator:
             if not todo:
                 continue
             if hasattr(authenticator, "authenticate_batch"):
-                results = authenticator.authenticate_batch([deepcopy(reqs[k]) for k in todo])
+                # the reference deep-copies per authenticator (req_authenticator.py:39) so a
+                # plugin cannot alter the request; the stock batch path never mutates it
+                ro = getattr(authenticator, "batch_reads_only", None)
+                copy = (lambda r: r) if (ro is not None and ro()) else deepcopy
+                results = authenticator.authenticate_batch([copy(reqs[k]) for k in todo])
             else:
                 results = []
                 for k in todo:

@@ -127,3 +127,62 @@ def test_pack_open_batch_positional_split():
         _edvhost.pack_open_batch([(b"x" * 64, b"", b"k" * 31)])
     with pytest.raises(ValueError):
         edv.open_batch([(b"x" * 64, b"", b"k" * 31)])
+
+
+def test_core_fast_path_equals_python_plan(monkeypatch):
+    """prep_core_batch (native) vs the Python plan vs sequential authenticate on
+    every key form and failure the single-signature path can meet."""
+    import test_authn_host as H
+    from indy_plenum_amd import client_authn
+    from indy_plenum_amd.client_authn import CoreAuthNr
+    monkeypatch.setattr(edv, "open_batch", H.oracle_open_batch)
+    r = random.Random(9)
+    crypt = H.Signer(seed=b"C" * 32)                        # cryptonym: idr = full verkey
+    full = H.Signer(identifier="V4SGRU86Z58d6TV7PBUe6f", seed=b"F" * 32)
+    abbr = H.Signer(seed=b"B" * 32)
+    abbr.identifier = base58.b58encode(abbr.pk[:16]).decode()
+    auth = CoreAuthNr()
+    auth.addIdr(crypt.identifier, "")                      # empty verkey -> the identifier itself
+    auth.addIdr(full.identifier, full.verkey)
+    auth.addIdr(abbr.identifier, "~" + base58.b58encode(abbr.pk[16:]).decode())
+    auth.addIdr("BadAbbr1111111111111111", "~0OIl")        # invalid abbreviation
+    auth.addIdr("HexKey", abbr.pk.hex())                  # hex-encoded 32-byte key
+    auth.addIdr("NoKey", None)
+    auth.clients["EmptyNym"] = {}
+    reqs = []
+    for i in range(400):
+        s = r.choice([crypt, full, abbr])
+        req = {"identifier": s.identifier, "reqId": i, "operation": {"type": "1", "n": i}, "protocolVersion": 2}
+        kind = r.randrange(12)
+        if kind == 0:
+            req["identifier"] = r.choice(["BadAbbr1111111111111111", "HexKey", "NoKey", "EmptyNym", "Unknown9"])
+        if kind == 1:
+            req["signature"] = "0OIl"
+        elif kind == 2:
+            req["signature"] = ""
+        elif kind == 3:
+            req["identifier"] = ""
+        elif kind == 4:
+            req["signature"] = s.sign({**req, "reqId": -1})
+        elif kind == 5:
+            req["signature"] = s.sign(req) + "  "           # trailing whitespace is stripped by b58decode
+        elif kind == 6:
+            req["fees"] = [1, 2]                          # excluded from the signing bytes
+            req["signature"] = s.sign({k: v for k, v in req.items() if k != "fees"})
+        elif kind == 7:
+            req["signature"] = s.sign(req)
+            req["signatures"] = {"other": "x"}            # ignored when identifier + signature are set
+        else:
+            req["signature"] = s.sign(req)
+        reqs.append(req)
+    seq = [H.outcome(lambda q=q: auth.authenticate(dict(q))) for q in reqs]
+    norm = lambda res: [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x)
+                        for x in res]
+    fast = norm(auth.authenticate_batch(reqs))
+    assert sum(1 for x in _edvhost.prep_core_batch(reqs, auth.clients, auth.excluded_from_signing)
+               if x is not None) > 150
+    monkeypatch.setattr(client_authn, "_edvhost", None)
+    slow = norm(auth.authenticate_batch(reqs))
+    assert fast == slow == seq
+    assert {o[0] if o[0] == "ok" else o[1] for o in seq} >= {"ok", "InsufficientCorrectSignatures",
+                                                            "InvalidSignatureFormat", "UnknownIdentifier"}
