@@ -288,27 +288,34 @@ class CoreAuthMixin:
         prepared natively in one call (_edvhost.prep_core_batch, row f-1); every
         other request goes through the Python plan, which raises exactly what
         the reference raises."""
-        out = [None] * len(reqs)
+        n = len(reqs)
+        out = [None] * n
         fast = self._native_prep(reqs, verifier)
-        jobs, plans, where = [], [], []
-        for k, req in enumerate(reqs):
-            pre = fast[k] if fast is not None else None
-            if pre is not None:
-                idr, sig, ser, pk = pre
-                # threshold None -> 1 signature; replay gives [idr] or InsufficientCorrectSignatures(0, 1)
-                plans.append(_Plan(1, [(idr, None, sig, ser, len(jobs))]))
-                jobs.append((sig, ser, pk))
-                where.append(k)
+        if fast is None:
+            fast = [None] * n
+        # fast requests: jobs 0..F-1, result [idr] or InsufficientCorrectSignatures(0, 1)
+        # (threshold None -> 1 signature), exactly what the replay of their plan gives
+        fast_idx = [k for k in range(n) if fast[k] is not None]
+        jobs = [fast[k][1:] for k in fast_idx]
+        plans, where = [], []
+        for k in range(n):
+            if fast[k] is not None:
                 continue
             try:
-                to_serialize, signatures = self._prepare(req)
+                to_serialize, signatures = self._prepare(reqs[k])
             except Exception as ex:
                 out[k] = ex
                 continue
             plans.append(self._plan_multi(to_serialize, signatures, None, verifier or DidVerifier, jobs))
             where.append(k)
-        for k, res in zip(where, self._run_plans(plans, jobs)):
-            out[k] = res
+        verdicts = edv.open_batch(jobs) if jobs else []
+        for j, k in enumerate(fast_idx):
+            out[k] = [fast[k][0]] if verdicts[j] else InsufficientCorrectSignatures(0, 1)
+        for k, plan in zip(where, plans):
+            try:
+                out[k] = self._replay(plan, verdicts)
+            except Exception as ex:
+                out[k] = ex
         return out
 
     def _native_prep(self, reqs, verifier):

@@ -45,54 +45,74 @@ inline bool str_space(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13) || (c 
 inline bool bytes_space(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }
 
 // base58 text -> bytes (base58 1.0.0 b58decode).  false = not handled here.
+// The magnitude is built in 32-bit limbs, five base-58 digits (58^5 < 2^32) per
+// multiply-add pass.
 bool b58_decode(const uint8_t* s, size_t n, bool is_str, std::string* out) {
   while (n && (is_str ? str_space(s[n - 1]) : bytes_space(s[n - 1]))) n--;
   size_t ones = 0;
   while (ones < n && s[ones] == '1') ones++;
   // b58decode_int strips trailing bytes-whitespace again (a no-op after the above
   // for str input; for bytes input it already happened)
-  std::vector<uint8_t> be;  // big-endian magnitude
-  be.reserve(n);
-  for (size_t i = ones; i < n; i++) {
-    const int d = g_index[s[i]];
-    if (d < 0) return false;
-    uint32_t carry = uint32_t(d);
-    for (size_t k = be.size(); k-- > 0;) {
-      const uint32_t v = uint32_t(be[k]) * 58u + carry;
-      be[k] = uint8_t(v);
-      carry = v >> 8;
+  std::vector<uint32_t> limb;  // little-endian 32-bit limbs of the integer
+  limb.reserve((n - ones) / 5 + 2);
+  size_t i = ones;
+  while (i < n) {
+    uint32_t chunk = 0, mul = 1;
+    for (int k = 0; k < 5 && i < n; k++, i++) {
+      const int d = g_index[s[i]];
+      if (d < 0) return false;
+      chunk = chunk * 58u + uint32_t(d);
+      mul *= 58u;
     }
-    while (carry) {
-      be.insert(be.begin(), uint8_t(carry));
-      carry >>= 8;
+    uint64_t carry = chunk;
+    for (auto& l : limb) {
+      const uint64_t v = uint64_t(l) * mul + carry;
+      l = uint32_t(v);
+      carry = v >> 32;
     }
+    if (carry) limb.push_back(uint32_t(carry));
   }
-  size_t lead = 0;  // to_bytes of the integer has no leading zero bytes
-  while (lead < be.size() && be[lead] == 0) lead++;
   out->assign(ones, '\0');
-  out->append(reinterpret_cast<const char*>(be.data()) + lead, be.size() - lead);
+  bool lead = true;  // to_bytes of the integer has no leading zero bytes
+  for (size_t k = limb.size(); k-- > 0;)
+    for (int b = 3; b >= 0; b--) {
+      const char c = char(limb[k] >> (8 * b));
+      if (lead && c == 0) continue;
+      lead = false;
+      out->push_back(c);
+    }
   return true;
 }
 
-// bytes -> base58 text (base58 1.0.0 b58encode)
+// bytes -> base58 text (base58 1.0.0 b58encode): big-endian 32-bit limbs,
+// divided by 58^5 per pass (five digits at a time).
 std::string b58_encode(const uint8_t* v, size_t n) {
   size_t zeros = 0;
   while (zeros < n && v[zeros] == 0) zeros++;
-  std::vector<uint8_t> digits;  // little-endian base-58 digits
-  for (size_t i = zeros; i < n; i++) {
-    uint32_t carry = v[i];
-    for (auto& d : digits) {
-      const uint32_t x = uint32_t(d) * 256u + carry;
-      d = uint8_t(x % 58u);
-      carry = x / 58u;
+  const size_t len = n - zeros;
+  std::vector<uint32_t> num((len + 3) / 4, 0);  // big-endian limbs
+  for (size_t i = 0; i < len; i++) {
+    const size_t pos = len - 1 - i;  // byte significance
+    num[num.size() - 1 - pos / 4] |= uint32_t(v[zeros + i]) << (8 * (pos % 4));
+  }
+  std::string rev;  // digits, least significant first
+  size_t first = 0;
+  while (first < num.size()) {
+    uint64_t rem = 0;
+    for (size_t k = first; k < num.size(); k++) {
+      const uint64_t cur = (rem << 32) | num[k];
+      num[k] = uint32_t(cur / 656356768u);  // 58^5
+      rem = cur % 656356768u;
     }
-    while (carry) {
-      digits.push_back(uint8_t(carry % 58u));
-      carry /= 58u;
+    while (first < num.size() && num[first] == 0) first++;
+    for (int d = 0; d < 5; d++) {
+      if (first >= num.size() && rem == 0) break;  // no leading zero digits
+      rev.push_back(kAlphabet[rem % 58u]);
+      rem /= 58u;
     }
   }
   std::string s(zeros, '1');
-  for (size_t k = digits.size(); k-- > 0;) s.push_back(kAlphabet[digits[k]]);
+  s.append(rev.rbegin(), rev.rend());
   return s;
 }
 
@@ -163,7 +183,13 @@ int ser(PyObject* obj, int level, PyObject* ignore, std::string& out) {
     r = append_str(obj, out);
   } else if (PyDict_Check(obj)) {
     // keys (minus the top-level ignore list), sorted; str keys only here
-    std::vector<std::pair<std::string, PyObject*>> items;
+    struct Item {
+      const char* k;  // UTF-8 of the key object ko
+      size_t n;
+      PyObject* ko;
+      PyObject* v;
+    };
+    std::vector<Item> items;
     PyObject *k, *v;
     Py_ssize_t pos = 0;
     while (r == 1 && PyDict_Next(obj, &pos, &k, &v)) {
@@ -176,23 +202,27 @@ int ser(PyObject* obj, int level, PyObject* ignore, std::string& out) {
       Py_ssize_t n;
       const char* u = PyUnicode_AsUTF8AndSize(k, &n);
       if (!u) { PyErr_Clear(); r = 0; break; }
-      Py_INCREF(v);  // str() of a value may run Python code: hold the values
-      items.emplace_back(std::string(u, size_t(n)), v);
+      Py_INCREF(k);  // str() of a value may run Python code: hold keys and values
+      Py_INCREF(v);
+      items.push_back(Item{u, size_t(n), k, v});
     }
     if (r == 1) {
       // UTF-8 byte order == code point order == Python's str sort
-      std::sort(items.begin(), items.end(),
-                [](const std::pair<std::string, PyObject*>& a, const std::pair<std::string, PyObject*>& b) {
-                  return a.first < b.first;
-                });
+      std::sort(items.begin(), items.end(), [](const Item& a, const Item& b) {
+        const int c = memcmp(a.k, b.k, a.n < b.n ? a.n : b.n);
+        return c != 0 ? c < 0 : a.n < b.n;
+      });
       for (size_t i = 0; r == 1 && i < items.size(); i++) {
         if (i) out.push_back('|');
-        out += items[i].first;
+        out.append(items[i].k, items[i].n);
         out.push_back(':');
-        r = ser(items[i].second, level + 1, nullptr, out);
+        r = ser(items[i].v, level + 1, nullptr, out);
       }
     }
-    for (auto& it : items) Py_DECREF(it.second);
+    for (auto& it : items) {
+      Py_DECREF(it.ko);
+      Py_DECREF(it.v);
+    }
   } else if (PyList_Check(obj)) {
     const Py_ssize_t n = PyList_GET_SIZE(obj);
     for (Py_ssize_t i = 0; r == 1 && i < n; i++) {

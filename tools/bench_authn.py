@@ -78,8 +78,20 @@ def phases():
             "replay_s": t1 - t["gpu_done"]}
 
 
+def run_req_authenticator():
+    from indy_plenum_amd.req_authenticator import ReqAuthenticator
+    ra = ReqAuthenticator()
+    ra.register_authenticator(auth)
+    t0 = time.perf_counter()
+    res = ra.authenticate_batch(reqs)
+    dt = time.perf_counter() - t0
+    assert all(x == {r["identifier"]} for x, r in zip(res, reqs))
+    return dt
+
+
 run_batch()
 native = min(run_batch() for _ in range(3))
+native_ra = min(run_req_authenticator() for _ in range(3))
 ph_native = phases()
 base58._native = signing_serializer._native = None  # force the Python restatements
 python_prep = min(run_batch() for _ in range(2))
@@ -118,7 +130,8 @@ if sodium is not None:
     cpu = k / (time.perf_counter() - t0)
 
 print(json.dumps({"metric": "authenticated NYM requests/s (CoreAuthNr.authenticate_batch, 1 GPU)", "n": N,
-                  "native_prep_req_per_s": N / native, "python_prep_req_per_s": N / python_prep,
+                  "native_prep_req_per_s": N / native,
+                  "req_authenticator_native_req_per_s": N / native_ra, "python_prep_req_per_s": N / python_prep,
                   "phases_native": ph_native, "phases_python": ph_python,
                   "cpu_reference_chain_req_per_s": cpu,
                   "cpu_reference_chain": "sequential CoreAuthNr.authenticate, Python restatement + libsodium "

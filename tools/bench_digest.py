@@ -3,7 +3,8 @@
 the host, same messages.  Prints one JSON line.
 
 Work per message: ceil((m + 9) / 64) SHA-256 compressions; one compression is
-counted as 64 rounds x ~40 + 48 schedule steps x ~16 = ~3,300 INT32 ops (the
+counted as 64 rounds x 23 (Sigma1 5, Ch 3, T1 4 adds, Sigma0 5, Maj 4, 2 adds)
++ 48 schedule steps x 13 (sigma0 5, sigma1 5, 3 adds) = 2,096 INT32 ops (the
 same accounting style as SURVEY.md section 8d's SHA-512 term).
 """
 import hashlib
@@ -39,7 +40,7 @@ k = min(n, 4096)
 for i in range(k):
     assert got[i].tobytes() == hashlib.sha256(msgs[off[i]:off[i + 1]].tobytes()).digest()
 blocks = (m + 9 + 63) // 64
-ops = n * blocks * 3300
+ops = n * blocks * 2096
 t1 = time.perf_counter()
 reps = 0
 while time.perf_counter() - t1 < 3.0:
