@@ -1,0 +1,261 @@
+"""A minimal in-process n-node pool for end-to-end measurement of the
+authentication path (Alpha-Delta under a
+client-request flood).  The reference pool cannot run in this image (zmq,
+rocksdb, indy-crypto, libindy and Python <= 3.6 are absent), so this harness
+keeps exactly the parts of the Node message flow that decide how often and where
+request signatures are verified, and reduces the rest to message counting:
+
+  client REQUEST to every node        plenum/server/node.py:1646-1743 (verify)
+    -> processRequest: record, PROPAGATE to all   node.py:2093-2143,
+                                                  propagator.py:165-183, 251-261
+  PROPAGATE from a peer               node.py:1553-1620 (verify again),
+    -> processPropagate: vote, propagate once     node.py:2183-2230
+  f+1 PROPAGATE votes -> finalised, forwarded     propagator.py:200-249
+  master replica 3PC: the primary batches finalised requests into a
+    PRE-PREPARE, PREPARE quorum n-f-1, COMMIT quorum n-f, ordered in
+    ppSeqNo order                                 plenum/server/replica.py
+  node-to-node messages are JSON-encoded and flushed once per prod per peer
+    as one batch                                  node.py:1049 flushOutBoxes
+
+Not modelled (out of scope): view change, checkpoints,
+catch-up, BLS multi-signatures, ledgers/state execution, client replies.
+
+Each node authenticates through a ReqAuthenticator; `batched=True` routes a
+prod's client REQUESTs and PROPAGATEs through ONE authenticate_batch call
+(node_integration.authenticate_prod), `batched=False` is the reference's
+one-message-at-a-time verifySignature.  Request keys are Request.getDigest
+(request.py:71-72) values computed by `digest_fn`.
+"""
+import hashlib
+import json
+import time
+from collections import deque
+
+from .node_integration import DEFAULT_LISTENER_QUOTA, authenticate_prod, failed
+from .signing_serializer import serialize_msg_for_signing
+from .digest import signing_state
+
+NAMES = ("Alpha", "Beta", "Gamma", "Delta", "Epsilon", "Zeta", "Eta", "Theta")
+
+
+def cpu_digests(reqs):
+    """Request.getDigest on the host (hashlib), one request at a time."""
+    return [hashlib.sha256(serialize_msg_for_signing(signing_state(r))).hexdigest() for r in reqs]
+
+
+class _ReqState:
+    __slots__ = ("votes", "propagated", "forwarded")
+
+    def __init__(self):
+        self.votes = set()
+        self.propagated = False
+        self.forwarded = False
+
+
+class PoolNode:
+    def __init__(self, name, peers, authenticator, f, batched=True, digest_fn=cpu_digests,
+                 client_quota=DEFAULT_LISTENER_QUOTA, node_quota=DEFAULT_LISTENER_QUOTA, max_batch=1000):
+        self.name, self.peers, self.auth, self.f = name, list(peers), authenticator, f
+        self.n = len(self.peers) + 1
+        self.batched, self.digest_fn = batched, digest_fn
+        self.client_quota, self.node_quota, self.max_batch = client_quota, node_quota, max_batch
+        self.client_inbox = deque()   # JSON text of client REQUESTs
+        self.node_inbox = deque()     # (frm, JSON text of one flushed batch)
+        self.outbox = {p: [] for p in self.peers}
+        self.requests = {}            # key -> _ReqState
+        self.ordered_keys = set()
+        self.finalised = deque()      # finalised keys not yet in a PRE-PREPARE (primary)
+        self.finalised_set = set()
+        self.is_primary = False
+        # master replica state
+        self.pp = {}                  # ppSeqNo -> list of keys
+        self.pp_waiting = []          # ppSeqNos received but not all requests finalised yet
+        self.prepares = {}            # ppSeqNo -> set of senders
+        self.commits = {}             # ppSeqNo -> set of senders
+        self.sent_prepare, self.sent_commit = set(), set()
+        self.last_pp = 0
+        self.last_ordered = 0
+        # counters
+        self.ordered = 0
+        self.nacks = 0
+        self.bad_propagates = 0
+        self.verifies = 0
+        self.auth_calls = 0
+        self.busy_s = 0.0
+
+    # ------------------------------------------------------------------ I/O
+    def send_all(self, msg):
+        for p in self.peers:
+            self.outbox[p].append(msg)
+
+    def flush(self, pool):
+        for p, msgs in self.outbox.items():
+            if msgs:
+                pool.nodes[p].node_inbox.append((self.name, json.dumps(msgs)))
+                self.outbox[p] = []
+
+    # ------------------------------------------------------------------ prod
+    def prod(self, pool):
+        t0 = time.perf_counter()
+        props, three_pc = [], []
+        for _ in range(min(self.node_quota, len(self.node_inbox))):
+            frm, blob = self.node_inbox.popleft()
+            for m in json.loads(blob):
+                (props if m["op"] == "PROPAGATE" else three_pc).append((m, frm))
+        clients = [(json.loads(self.client_inbox.popleft()), "client")
+                   for _ in range(min(self.client_quota, len(self.client_inbox)))]
+        if props or clients:
+            keys = self.digest_fn([m["request"] for m, _ in props] + [m for m, _ in clients])
+            self._keys = iter(keys)
+            self.verifies += len(props) + len(clients)
+            self.auth_calls += 1 if self.batched else len(props) + len(clients)
+            authenticate_prod(self.auth, clients, props, self._on_client, self._on_propagate, self.batched)
+        for m, frm in three_pc:
+            getattr(self, "_on_" + m["op"])(m, frm)
+        self._service_replica()
+        self.flush(pool)
+        self.busy_s += time.perf_counter() - t0
+        return len(props) + len(clients) + len(three_pc)
+
+    # ------------------------------------------------------- requests
+    def _on_client(self, req, frm, outcome):
+        key = next(self._keys)
+        if failed(outcome):
+            self.nacks += 1           # handleInvalidClientMsg: REQNACK to the client
+            return
+        if key in self.ordered_keys:
+            return                    # already ordered: the reference replies from the ledger
+        self._record_and_propagate(key, req, frm)
+
+    def _on_propagate(self, msg, frm, outcome):
+        key = next(self._keys)
+        if failed(outcome):
+            self.bad_propagates += 1  # SuspiciousNode
+            return
+        if key in self.ordered_keys:
+            return
+        st = self.requests.get(key)
+        if st is None:
+            st = self.requests[key] = _ReqState()
+        st.votes.add(frm)
+        self._record_and_propagate(key, msg["request"], msg.get("senderClient"))
+
+    def _record_and_propagate(self, key, req, client):
+        st = self.requests.get(key)
+        if st is None:
+            st = self.requests[key] = _ReqState()
+        if not st.propagated:
+            st.propagated = True
+            st.votes.add(self.name)
+            self.send_all({"op": "PROPAGATE", "request": req, "senderClient": client})
+        if not st.forwarded and len(st.votes) >= self.f + 1:   # Quorums.propagate = f + 1
+            st.forwarded = True
+            self.finalised_set.add(key)
+            if self.is_primary:
+                self.finalised.append(key)
+
+    # ------------------------------------------------------- master replica (3PC)
+    def _service_replica(self):
+        if self.is_primary:
+            while self.finalised:
+                keys = [self.finalised.popleft() for _ in range(min(self.max_batch, len(self.finalised)))]
+                self.last_pp += 1
+                self.pp[self.last_pp] = keys
+                self.send_all({"op": "PREPREPARE", "ppSeqNo": self.last_pp, "reqIdr": keys})
+        still = []
+        for s in self.pp_waiting:
+            if all(k in self.finalised_set for k in self.pp[s]):
+                self._send_prepare(s)
+            else:
+                still.append(s)
+        self.pp_waiting = still
+        self._try_order()
+
+    def _on_PREPREPARE(self, m, frm):
+        s = m["ppSeqNo"]
+        self.pp[s] = m["reqIdr"]
+        self.pp_waiting.append(s)
+
+    def _send_prepare(self, s):
+        if s not in self.sent_prepare:
+            self.sent_prepare.add(s)
+            self.prepares.setdefault(s, set()).add(self.name)
+            self.send_all({"op": "PREPARE", "ppSeqNo": s})
+            self._check_prepared(s)
+
+    def _on_PREPARE(self, m, frm):
+        s = m["ppSeqNo"]
+        self.prepares.setdefault(s, set()).add(frm)
+        self._check_prepared(s)
+
+    def _check_prepared(self, s):
+        # prepare quorum n - f - 1 (the primary sends none); a non-primary also needs its own PREPARE
+        if s in self.sent_commit or s not in self.pp:
+            return
+        if not self.is_primary and s not in self.sent_prepare:
+            return
+        others = len(self.prepares.get(s, set()) - {self.name})
+        need = self.n - self.f - 1
+        if others + (0 if self.is_primary else 1) >= need:
+            self.sent_commit.add(s)
+            self.commits.setdefault(s, set()).add(self.name)
+            self.send_all({"op": "COMMIT", "ppSeqNo": s})
+
+    def _on_COMMIT(self, m, frm):
+        self.commits.setdefault(m["ppSeqNo"], set()).add(frm)
+
+    def _try_order(self):
+        while True:
+            s = self.last_ordered + 1
+            if s not in self.sent_commit or len(self.commits.get(s, ())) < self.n - self.f:
+                return
+            keys = self.pp.pop(s)
+            for k in keys:
+                self.ordered_keys.add(k)
+                self.requests.pop(k, None)
+                self.finalised_set.discard(k)
+            self.ordered += len(keys)
+            self.last_ordered = s
+            self.prepares.pop(s, None)
+            self.commits.pop(s, None)
+
+
+class Pool:
+    """n nodes (f = (n - 1) // 3), primary = the first; `auth_factory(name)`
+    returns each node's ReqAuthenticator."""
+
+    def __init__(self, auth_factory, n=4, batched=True, digest_fn=cpu_digests, **node_kw):
+        names = NAMES[:n]
+        f = (n - 1) // 3
+        self.nodes = {nm: PoolNode(nm, [p for p in names if p != nm], auth_factory(nm), f, batched, digest_fn,
+                                   **node_kw) for nm in names}
+        self.nodes[names[0]].is_primary = True
+
+    def submit(self, reqs):
+        """A client flood: every request sent to every node (as the client does)."""
+        for r in reqs:
+            blob = json.dumps(r)
+            for node in self.nodes.values():
+                node.client_inbox.append(blob)
+
+    def run(self, expect, max_idle_rounds=50):
+        """prod every node round-robin until `expect` requests are ordered on
+        every node; returns the wall-clock seconds."""
+        t0 = time.perf_counter()
+        idle = 0
+        while min(nd.ordered for nd in self.nodes.values()) < expect:
+            work = sum(nd.prod(self) for nd in self.nodes.values())
+            idle = 0 if work else idle + 1
+            if idle > max_idle_rounds:
+                raise RuntimeError("pool stalled: ordered %s of %d" % ([nd.ordered for nd in self.nodes.values()],
+                                                                      expect))
+        return time.perf_counter() - t0
+
+    def stats(self, wall_s, n_reqs):
+        nodes = list(self.nodes.values())
+        busy = max(nd.busy_s for nd in nodes)
+        return {"ordered_per_node": [nd.ordered for nd in nodes], "nacks_per_node": [nd.nacks for nd in nodes],
+                "bad_propagates": sum(nd.bad_propagates for nd in nodes),
+                "verifies": sum(nd.verifies for nd in nodes), "auth_calls": sum(nd.auth_calls for nd in nodes),
+                "wall_s": wall_s, "ordered_req_per_s_one_process": n_reqs / wall_s,
+                "max_node_busy_s": busy, "ordered_req_per_s_parallel_nodes": n_reqs / busy}

@@ -1,0 +1,72 @@
+"""Row f-2 harness logic on CPU: a 4-node pool (Alpha..Delta) under a small
+client flood orders every valid request exactly once on every node and NACKs
+the invalid ones, with one-message-at-a-time verification (the reference's
+verifySignature loop) and with prod-batched authenticate_batch (one device call
+per prod); the device call is the oracle here (the GPU run is in
+tests/test_gpu_authn.py / tools/bench_pool.py)."""
+import random
+
+import pytest
+
+import test_authn_host as H
+from indy_plenum_amd import edv
+from indy_plenum_amd.client_authn import CoreAuthNr
+from indy_plenum_amd.pool import Pool, cpu_digests
+from indy_plenum_amd.req_authenticator import ReqAuthenticator
+
+
+def flood(n_valid=60, n_bad_sig=10, n_unknown=5, seed=3):
+    r = random.Random(seed)
+    signers = [H.Signer(seed=bytes([k + 1]) * 32) for k in range(6)]
+    reqs, valid = [], []
+    for i in range(n_valid + n_bad_sig + n_unknown):
+        s = r.choice(signers)
+        req = {"identifier": s.identifier, "reqId": 1539648000000000 + i, "protocolVersion": 2,
+               "operation": {"type": "1", "dest": "D%d" % i}}
+        if i < n_valid:
+            req["signature"] = s.sign(req)
+            valid.append(req)
+        elif i < n_valid + n_bad_sig:
+            req["signature"] = s.sign({**req, "reqId": 7})
+        else:
+            req["identifier"] = "Unknown%d" % i
+            req["signature"] = s.sign(req)
+        reqs.append(req)
+    r.shuffle(reqs)
+    return signers, reqs, valid
+
+
+def factory(signers):
+    def make(_name):
+        a = CoreAuthNr()
+        for s in signers:
+            a.addIdr(s.identifier, s.verkey)
+        ra = ReqAuthenticator()
+        ra.register_authenticator(a)
+        return ra
+    return make
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_pool_orders_every_valid_request_once(batched, monkeypatch):
+    calls = []
+
+    def oracle(items, device_mask=0):
+        items = list(items)
+        calls.append(len(items))
+        return H.oracle_open_batch(items)
+    monkeypatch.setattr(edv, "open_batch", oracle)
+    signers, reqs, valid = flood()
+    pool = Pool(factory(signers), n=4, batched=batched, digest_fn=cpu_digests, client_quota=16, max_batch=7)
+    pool.submit(reqs)
+    wall = pool.run(len(valid))
+    st = pool.stats(wall, len(valid))
+    assert st["ordered_per_node"] == [len(valid)] * 4
+    assert st["nacks_per_node"] == [len(reqs) - len(valid)] * 4
+    assert st["bad_propagates"] == 0
+    keys = [nd.ordered_keys for nd in pool.nodes.values()]
+    assert all(k == keys[0] for k in keys) and keys[0] == set(cpu_digests(valid))
+    # every node verifies every request once from the client and once per peer's PROPAGATE
+    assert st["verifies"] == 4 * len(reqs) + 4 * 3 * len(valid)
+    if batched:
+        assert st["auth_calls"] < st["verifies"] / 4   # one authenticate_batch per prod

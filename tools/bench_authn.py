@@ -10,7 +10,6 @@ Python restatement, the phase split, and the reference's own CPU chain
 ctypes, i.e. what libnacl does) timed on the same host, 1 thread like the
 Node's Looper.  Keys/signatures come from the GPU batch signer.
 """
-import ctypes
 import json
 import os
 import sys
@@ -23,7 +22,6 @@ sys.path.insert(0, ROOT)
 from indy_plenum_amd import base58, edv, signing_serializer  # noqa: E402
 from indy_plenum_amd.client_authn import CoreAuthNr  # noqa: E402
 from indy_plenum_amd.signing_serializer import serialize_msg_for_signing  # noqa: E402
-from indy_plenum_amd.verifier import DidVerifier, Verifier  # noqa: E402
 
 N = int(os.environ.get("N", 10000))
 rng = np.random.default_rng(0xC1)
@@ -98,35 +96,16 @@ python_prep = min(run_batch() for _ in range(2))
 ph_python = phases()
 
 # the reference's CPU chain: Python + libsodium per request (crypto_sign_open(sig + msg, pk))
-sodium = None
-for path in ("/opt/conda/lib/libsodium.so.23", "libsodium.so.23", "libsodium.so"):
-    try:
-        sodium = ctypes.CDLL(path)
-        break
-    except OSError:
-        continue
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import sodium_ref  # noqa: E402
 cpu = None
-if sodium is not None:
-    sodium.sodium_init()
-
-    class SodiumVerifier(Verifier):
-        """DidVerifier key derivation + crypto_sign_open, as libnacl does it."""
-
-        def __init__(self, verkey, identifier=None):
-            self.pk = DidVerifier(verkey, identifier).batch_key()
-
-        def verify(self, sig, msg):
-            sm = bytes(sig) + bytes(msg)
-            m = ctypes.create_string_buffer(len(sm))
-            mlen = ctypes.c_ulonglong(0)
-            return sodium.crypto_sign_open(m, ctypes.byref(mlen), sm, ctypes.c_ulonglong(len(sm)), self.pk) == 0
-
+if sodium_ref.sodium() is not None:
     k = min(N, 3000)
     cpu_auth = CoreAuthNr()
     cpu_auth.clients = auth.clients
     t0 = time.perf_counter()
     for r in reqs[:k]:
-        assert cpu_auth.authenticate(r, verifier=SodiumVerifier) == [r["identifier"]]
+        assert cpu_auth.authenticate(r, verifier=sodium_ref.SodiumVerifier) == [r["identifier"]]
     cpu = k / (time.perf_counter() - t0)
 
 print(json.dumps({"metric": "authenticated NYM requests/s (CoreAuthNr.authenticate_batch, 1 GPU)", "n": N,

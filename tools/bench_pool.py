@@ -1,0 +1,94 @@
+"""Row f-2 / config C5: ordered requests/s of a 4-node pool (Alpha..Delta,
+indy-plenum_amd/pool.py) under a client flood of NYM requests, with
+  gpu_batched:   each prod's REQUESTs + PROPAGATEs authenticated by ONE
+                 ReqAuthenticator.authenticate_batch (GPU verify, native host
+                 prep) and request digests by one GPU SHA-256 batch;
+  cpu_reference: one verifySignature per message on libsodium (ctypes, as
+                 libnacl), pure-Python base58/serializer, hashlib digests --
+                 the reference Node's path.
+Same harness, quotas and 3PC batching in both.  All nodes run in one process
+(like the reference's test pool on one Looper); the 'parallel_nodes' rate
+divides by the busiest node's own time (nodes on separate hosts).
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from indy_plenum_amd import base58, digest, edv, signing_serializer  # noqa: E402
+from indy_plenum_amd.client_authn import CoreAuthNr  # noqa: E402
+from indy_plenum_amd.pool import Pool, cpu_digests  # noqa: E402
+from indy_plenum_amd.req_authenticator import ReqAuthenticator  # noqa: E402
+from indy_plenum_amd.signing_serializer import serialize_msg_for_signing  # noqa: E402
+import sodium_ref  # noqa: E402
+
+
+def make_flood(n, seed=0xC5):
+    rng = np.random.default_rng(seed)
+    seeds = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    pks, _ = edv.sign_arrays(seeds.tobytes(), b"\0" * 64, np.zeros(n + 1, dtype=np.uint64))
+    pks = pks.tobytes()
+    clients, reqs = {}, []
+    for i in range(n):
+        pk = pks[32 * i:32 * i + 32]
+        idr = base58.b58encode(pk[:16]).decode()
+        clients[idr] = "~" + base58.b58encode(pk[16:]).decode()
+        reqs.append({"identifier": idr, "reqId": 1539648000000000 + i, "protocolVersion": 2,
+                     "operation": {"type": "1", "dest": base58.b58encode(rng.bytes(16)).decode(),
+                                   "verkey": "~" + base58.b58encode(rng.bytes(16)).decode()}})
+    sers = [serialize_msg_for_signing(r) for r in reqs]
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(s) for s in sers])
+    _, sigs = edv.sign_arrays(seeds.tobytes(), b"".join(sers) + b"\0" * 64, off)
+    sigs = sigs.tobytes()
+    for i, r in enumerate(reqs):
+        r["signature"] = base58.b58encode(sigs[64 * i:64 * i + 64]).decode()
+    return clients, reqs
+
+
+def factory(clients, cls):
+    def make(_name):
+        a = cls()
+        for idr, vk in clients.items():
+            a.addIdr(idr, vk)
+        ra = ReqAuthenticator()
+        ra.register_authenticator(a)
+        return ra
+    return make
+
+
+def run(mode, clients, reqs):
+    if mode == "gpu_batched":
+        pool = Pool(factory(clients, CoreAuthNr), n=4, batched=True, digest_fn=digest.request_digests)
+    else:
+        pool = Pool(factory(clients, sodium_ref.SodiumCoreAuthNr), n=4, batched=False, digest_fn=cpu_digests)
+    native = base58._native
+    if mode == "cpu_reference":  # the reference's pure-Python base58 / serializer
+        base58._native = signing_serializer._native = None
+    try:
+        pool.submit(reqs)
+        wall = pool.run(len(reqs))
+    finally:
+        base58._native = signing_serializer._native = native
+    st = pool.stats(wall, len(reqs))
+    st["requests"] = len(reqs)
+    return st
+
+
+N = int(os.environ.get("N", 20000))
+N_CPU = int(os.environ.get("N_CPU", 2000))
+clients, reqs = make_flood(N)
+warm = run("gpu_batched", clients, reqs[:500])
+out = {"metric": "4-node pool ordered requests/s under a client flood (C5)", "n_nodes": 4, "f": 1,
+       "gpu_batched": run("gpu_batched", clients, reqs)}
+if sodium_ref.sodium() is not None:
+    out["cpu_reference"] = run("cpu_reference", clients, reqs[:N_CPU])
+    out["speedup_one_process"] = (out["gpu_batched"]["ordered_req_per_s_one_process"]
+                                  / out["cpu_reference"]["ordered_req_per_s_one_process"])
+    out["speedup_parallel_nodes"] = (out["gpu_batched"]["ordered_req_per_s_parallel_nodes"]
+                                     / out["cpu_reference"]["ordered_req_per_s_parallel_nodes"])
+print(json.dumps(out))
