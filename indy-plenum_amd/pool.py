@@ -52,10 +52,32 @@ class _ReqState:
         self.forwarded = False
 
 
+class _TimedAuth:
+    """ReqAuthenticator proxy adding the time spent inside it to node.auth_s."""
+
+    def __init__(self, auth, node):
+        self._auth, self._node = auth, node
+
+    def authenticate(self, req):
+        t = time.perf_counter()
+        try:
+            return self._auth.authenticate(req)
+        finally:
+            self._node.auth_s += time.perf_counter() - t
+
+    def authenticate_batch(self, reqs):
+        t = time.perf_counter()
+        try:
+            return self._auth.authenticate_batch(reqs)
+        finally:
+            self._node.auth_s += time.perf_counter() - t
+
+
 class PoolNode:
     def __init__(self, name, peers, authenticator, f, batched=True, digest_fn=cpu_digests,
                  client_quota=DEFAULT_LISTENER_QUOTA, node_quota=DEFAULT_LISTENER_QUOTA, max_batch=1000):
-        self.name, self.peers, self.auth, self.f = name, list(peers), authenticator, f
+        self.name, self.peers, self.f = name, list(peers), f
+        self.auth = _TimedAuth(authenticator, self)
         self.n = len(self.peers) + 1
         self.batched, self.digest_fn = batched, digest_fn
         self.client_quota, self.node_quota, self.max_batch = client_quota, node_quota, max_batch
@@ -82,6 +104,7 @@ class PoolNode:
         self.verifies = 0
         self.auth_calls = 0
         self.busy_s = 0.0
+        self.auth_s = 0.0             # time inside request authentication and request digests
 
     # ------------------------------------------------------------------ I/O
     def send_all(self, msg):
@@ -105,7 +128,9 @@ class PoolNode:
         clients = [(json.loads(self.client_inbox.popleft()), "client")
                    for _ in range(min(self.client_quota, len(self.client_inbox)))]
         if props or clients:
+            ta = time.perf_counter()
             keys = self.digest_fn([m["request"] for m, _ in props] + [m for m, _ in clients])
+            self.auth_s += time.perf_counter() - ta
             self._keys = iter(keys)
             self.verifies += len(props) + len(clients)
             self.auth_calls += 1 if self.batched else len(props) + len(clients)
@@ -258,4 +283,5 @@ class Pool:
                 "bad_propagates": sum(nd.bad_propagates for nd in nodes),
                 "verifies": sum(nd.verifies for nd in nodes), "auth_calls": sum(nd.auth_calls for nd in nodes),
                 "wall_s": wall_s, "ordered_req_per_s_one_process": n_reqs / wall_s,
-                "max_node_busy_s": busy, "ordered_req_per_s_parallel_nodes": n_reqs / busy}
+                "max_node_busy_s": busy, "ordered_req_per_s_parallel_nodes": n_reqs / busy,
+                "auth_share_of_node_time": sum(nd.auth_s for nd in nodes) / sum(nd.busy_s for nd in nodes)}
