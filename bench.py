@@ -8,9 +8,11 @@ fraction and the libsodium CPU baseline timed on the same box.
 A "step" = one pass of the verifier (prep + main kernels) over one batch of B
 synthetic signed requests resident in HBM (default B = 65,536 x 256-byte
 NYM-shaped messages, distinct signers: BASELINE.json configs[1]).  The K timed
-steps are submitted back to back on the library's two-stream pipeline (the
-prep kernel of step k+1 overlaps the main kernel of step k, double-buffered
-state); the strictly sequential rate is reported beside it.  With N > 1
+steps are enqueued back to back on the library stream, strictly in sequence
+(prep, main, prep, main, ...), so the kernel durations rocprofv3 reports for the
+run are the ones the roofline uses.  --pipeline times the library's two-stream
+pipeline instead (prep of step k+1 beside main of step k, double-buffered
+state; +1-3 %) and reports the sequential rate beside it.  With N > 1
 (launched by torch.distributed.run) every rank verifies its own B-request shard
 of the request index space: weak scaling, no collective on the data path; the
 per-request accept bytes are checked after the timed region.
@@ -117,7 +119,8 @@ def main():
     ap.add_argument("--msg-len", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pipeline", action="store_true", help="time steps strictly in sequence on one stream")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="time the two-stream pipelined submission (prep of step k+1 beside main of step k)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -156,16 +159,16 @@ def main():
 
     for _ in range(args.warmup):
         batch.verify()
-        batch.submit()
-    edv.pipeline_sync(dev)
+        if args.pipeline:
+            batch.submit()
+    if args.pipeline:
+        edv.pipeline_sync(dev)
     ok = batch.accept()
     assert ok.all(), "warm-up verify rejected %d valid signatures" % int((ok == 0).sum())
 
-    # Timed region: K steps submitted back to back on the library's two-stream
-    # pipeline (edv_verify_batch_dev_pipelined: the prep kernel of step k+1 runs
-    # beside the main kernel of step k, as for a continuous stream of client
-    # batches), closed by a pipeline sync.  Host launch latency never sits
-    # between steps.
+    # Timed region: K steps enqueued back to back (host launch latency never
+    # sits between steps), closed by a device sync; with --pipeline, on the
+    # library's two-stream pipeline (edv_verify_batch_dev_pipelined) instead.
     def timed(submit, drain):
         edv.sync(dev)
         drain()
@@ -178,16 +181,12 @@ def main():
         barrier()
         return max_over_ranks(t1 - t0)
 
-    if args.no_pipeline:
-        s = edv.stream(dev)
-        elapsed = timed(lambda: batch.verify(stream=s), lambda: edv.sync(dev))
-    else:
-        elapsed = timed(batch.submit, lambda: edv.pipeline_sync(dev))
+    s = edv.stream(dev)
+    seq_elapsed = timed(lambda: batch.verify(stream=s), lambda: edv.sync(dev))
+    elapsed = timed(batch.submit, lambda: edv.pipeline_sync(dev)) if args.pipeline else seq_elapsed
     ms_step = 1e3 * elapsed / args.steps
     total = n * world * args.steps
     value = total / elapsed
-    # the same steps strictly one after another on one stream (reported beside it)
-    seq_elapsed = timed(lambda: batch.verify(stream=edv.stream(dev)), lambda: edv.sync(dev))
 
     # per-kernel durations (HIP events on the kernels' own stream), same batch
     iters = max(3, min(args.steps, 10))
@@ -233,7 +232,7 @@ def main():
                      "ops_per_launch": MAIN_OPS * n, "kernel_ms": main_ms, "prep_kernel_ms": prep_ms,
                      "whole_path_frac": whole / PEAK_INT32},
         "all_accepted": bool(all_ok),
-        "timing": {"mode": "sequential" if args.no_pipeline else "pipelined (prep of step k+1 beside main of step k)",
+        "timing": {"mode": "pipelined (prep of step k+1 beside main of step k)" if args.pipeline else "sequential",
                    "sequential_ms_per_step": 1e3 * seq_elapsed / args.steps,
                    "sequential_value": n * world * args.steps / seq_elapsed},
     }
