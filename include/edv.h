@@ -121,6 +121,14 @@ int edv_profile_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uin
  * down to a multiple of 256).  Tuning/testing knob: verdicts never depend on it. */
 int edv_set_chunk(int device, uint64_t chunk);
 
+/* SHA-512 length buckets of the device paths (a counting sort of each chunk by
+ * block count, so a wave of the prep kernel hashes equally long messages):
+ * 0 = never (a caller whose messages all have one length saves three small
+ * launches per chunk), 1 = always, 2 = auto (default: on for device-resident
+ * batches; the host path buckets only when lengths differ).  Tuning knob:
+ * verdicts never depend on it. */
+int edv_set_length_buckets(int device, int mode);
+
 /*
  * Batch Ed25519 signing for synthetic load generation,
  * device-resident: seeds n x 32 B -> pks n x 32 B and detached sigs n x 64 B

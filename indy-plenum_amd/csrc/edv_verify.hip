@@ -329,6 +329,7 @@ struct DevCtx {
   int32_t* btab = nullptr;
   int32_t* comb = nullptr;         // signer comb table, built on first edv_sign_* call
   uint64_t chunk = kChunkDefault;  // EDV_CHUNK overrides (tests exercise chunk seams)
+  int length_buckets = 2;          // 0 never, 1 always, 2 auto (edv_set_length_buckets)
   ChunkBufs st;                    // state of the ordinary (one stream) path
   DevBuf sigs, pks, msgs, off, acc;
   // Pipelined submission (edv_verify_batch_dev_pipelined): two state sets, a
@@ -425,17 +426,23 @@ int launch_main(const VerifyArgs& va, hipStream_t s) {
   return 0;
 }
 
-static bool bucketing_enabled(bool want) {
+// Length buckets cost three small launches per chunk (memset, histogram,
+// scatter); a caller that knows its messages share one SHA-512 block count
+// turns them off with edv_set_length_buckets(device, 0).  Verdicts never depend on it.
+static bool bucketing_enabled(const DevCtx& c, bool want, bool host_path = false) {
   static const bool no_bucket = getenv("EDV_NO_BUCKET") != nullptr;  // A/B measurement knob
-  return want && !no_bucket;
+  if (no_bucket) return false;
+  if (host_path || c.length_buckets == 2) return want;  // the host path knows the lengths
+  return c.length_buckets == 1;
 }
 
 // Ordinary path: launch on ctx stream or the given stream; caller holds c.mu.
 // The batch is walked in chunks of c.chunk signatures: [length buckets,] prep
 // kernel, main kernel, all in stream order.
 int launch(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_off,
-           uint64_t msg_base, uint64_t n, uint8_t* d_accept, hipStream_t s, bool bucket = true) {
-  bucket = bucketing_enabled(bucket);
+           uint64_t msg_base, uint64_t n, uint8_t* d_accept, hipStream_t s, bool bucket = true,
+           bool host_path = false) {
+  bucket = bucketing_enabled(c, bucket, host_path);
   if (c.pipe_ready) {  // state set 0 of the pipeline is separate, but drain it so results stay ordered
     HIPOK(hipStreamSynchronize(c.sp), "pipeline sync");
     HIPOK(hipStreamSynchronize(c.sm), "pipeline sync");
@@ -472,7 +479,7 @@ int launch_pipelined(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, con
                      const uint64_t* d_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept) {
   int err;
   if ((err = pipe_init(c))) return err;
-  const bool bucket = bucketing_enabled(true);
+  const bool bucket = bucketing_enabled(c, true);
   HIPOK(hipEventRecord(c.inputs_ready, c.stream), "record");
   HIPOK(hipStreamWaitEvent(c.sp, c.inputs_ready, 0), "wait");
   for (uint64_t base = 0; base < n; base += c.chunk) {
@@ -520,7 +527,7 @@ int run_shard(int dev, const uint8_t* sigs, const uint8_t* pks, const uint8_t* m
   }
   if ((err = launch(*c, static_cast<uint8_t*>(c->sigs.p), static_cast<uint8_t*>(c->pks.p),
                     static_cast<uint8_t*>(c->msgs.p), static_cast<uint64_t*>(c->off.p), mbase, n,
-                    static_cast<uint8_t*>(c->acc.p), c->stream, varied)))
+                    static_cast<uint8_t*>(c->acc.p), c->stream, varied, true)))
     return err;
   HIPOK(hipMemcpyAsync(accept + lo, c->acc.p, n, hipMemcpyDeviceToHost, c->stream), "d2h accept");
   HIPOK(hipStreamSynchronize(c->stream), "stream sync");
@@ -787,6 +794,17 @@ int edv_set_chunk(int device, uint64_t chunk) {
   return 0;
 }
 
+int edv_set_length_buckets(int device, int mode) {
+  g_err.clear();
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  if (mode < 0 || mode > 2) return set_err(EDV_E_ARG, "length-bucket mode must be 0, 1 or 2");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->length_buckets = mode;
+  return 0;
+}
+
 int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
                           const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, int device,
                           int iters, float* ms_prep, float* ms_main) {
@@ -810,7 +828,7 @@ int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uin
   va.btab = c->btab;
   va.base = 0;
   uint32_t* hist = static_cast<uint32_t*>(c->st.bucket_ctr.p);
-  const bool bucket = bucketing_enabled(true);
+  const bool bucket = bucketing_enabled(*c, true);
   if (!bucket) va.st.perm = nullptr;
   va.n = n;
   const unsigned blocks = unsigned((n + kBlock - 1) / kBlock);

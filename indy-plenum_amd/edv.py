@@ -82,6 +82,8 @@ def lib():
         h.edv_stream.restype = ctypes.c_int
         h.edv_sync.argtypes = [ctypes.c_int]
         h.edv_sync.restype = ctypes.c_int
+        h.edv_set_length_buckets.argtypes = [ctypes.c_int, ctypes.c_int]
+        h.edv_set_length_buckets.restype = ctypes.c_int
         h.edv_set_chunk.argtypes = [ctypes.c_int, u64]
         h.edv_set_chunk.restype = ctypes.c_int
         h.edv_device_count.argtypes = []
@@ -114,6 +116,11 @@ def stream(device: int = 0) -> int:
 def sync(device: int = 0):
     """Wait for everything enqueued on the library stream of `device`."""
     _check(lib().edv_sync(device))
+
+
+def set_length_buckets(device: int, mode: int):
+    """SHA-512 length buckets on the device paths: 0 never, 1 always, 2 auto (default)."""
+    _check(lib().edv_set_length_buckets(device, mode))
 
 
 def set_chunk(device: int, chunk: int):

@@ -76,6 +76,8 @@ class DeviceBatch:
         self.d_accept = edv.DeviceBuffer(n, device)
         edv.sign_device(d_seeds.ptr, self.d_msgs.ptr, self.d_off.ptr, n, self.d_pks.ptr, self.d_sigs.ptr, device)
         d_seeds.free()
+        # one SHA-512 block count for the whole batch: no length buckets needed
+        edv.set_length_buckets(device, 0 if var_range is None else 2)
 
     def verify(self, stream=None):
         edv.verify_device(self.d_sigs.ptr, self.d_pks.ptr, self.d_msgs.ptr, self.d_off.ptr, self.n,
