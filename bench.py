@@ -114,7 +114,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=50, help="untimed steps first (clocks settle; ~50 ms)")
     ap.add_argument("--batch", type=int, default=65536, help="requests per GPU per step")
     ap.add_argument("--msg-len", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

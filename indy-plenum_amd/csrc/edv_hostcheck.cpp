@@ -57,6 +57,7 @@ void hc_fe_sq(const int32_t* f, int32_t* h) { from_fe(h, fe_sq(to_fe(f))); }
 void hc_fe_sq2(const int32_t* f, int32_t* h) { from_fe(h, fe_sq2(to_fe(f))); }
 void hc_fe_carry32(const int32_t* f, int32_t* h) { from_fe(h, fe_carry32(to_fe(f))); }
 void hc_fe_invert(const int32_t* f, int32_t* h) { from_fe(h, fe_invert(to_fe(f))); }
+void hc_fe_invert_safegcd(const int32_t* f, int32_t* h) { from_fe(h, fe_invert_safegcd(to_fe(f))); }
 void hc_fe_pow22523(const int32_t* f, int32_t* h) { from_fe(h, fe_pow22523(to_fe(f))); }
 void hc_fe_tobytes(const int32_t* f, uint8_t* out) { uint32_t w[8]; fe_tobytes(w, to_fe(f)); store_words(out, w, 8); }
 void hc_fe_frombytes(const uint8_t* in, int32_t* h) { uint32_t w[8]; load_words(w, in, 8); from_fe(h, fe_frombytes(w)); }

@@ -342,6 +342,148 @@ EDV_HD fe fe_pow22523(const fe& z) {
   return fe_mul(fe_sqn(t, 2), z);
 }
 
+// ------------------------------------------------ inversion by safegcd (V9)
+// z^-1 by Bernstein-Yang constant-time divsteps ("Fast constant-time gcd
+// computation and modular inversion", 2019), in the eta ("hddivstep") form with
+// 20 batches of 30 divsteps (600 >= the 590 proven sufficient for 256-bit
+// moduli), on signed 30-bit limbs.  About 13.5k instructions per lane against
+// ~30k for z^(p-2) (254 squarings + 11 products); every lane runs the same
+// fixed schedule, so the wave never diverges.
+//   f, g  the gcd pair (f = p, g = z), 9 signed limbs of 30 bits
+//   d, e  d*z = f and e*z = g (mod p) throughout; at the end g = 0, f = +-1
+struct s30 { int32_t v[9]; };
+// A masked limb is known non-negative, so LLVM widens it with zext; a signed x
+// zext 32x32 product then matches neither v_mad_i64_i32 nor v_mad_u64_u32 and
+// becomes a 64-bit multiply (mul_lo + mad_u64 + add).  Hiding the value range
+// keeps every limb product one v_mad_i64_i32.
+EDV_HD int32_t opaque_i32(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
+constexpr int32_t kM30 = 0x3fffffff;
+constexpr uint32_t kPInv30 = 0x179435e5u;  // p^-1 mod 2^30 (p = -19 mod 2^30)
+// p = -19 + 2^15 * 2^240 in signed-30 limbs: limb 0 = -19, limb 8 = 2^15, the rest 0.
+
+// 30 divsteps on the low 30 bits of f and g: returns the new eta and the
+// transition matrix [u v; q r] scaled by 2^30 ((f', g') = T (f, g) / 2^30).
+EDV_HD int32_t divsteps_30(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+#pragma unroll
+  for (int i = 0; i < 30; i++) {
+    uint32_t c1 = uint32_t(eta >> 31);   // eta < 0
+    const uint32_t c2 = 0u - (g & 1u);   // g odd
+    const uint32_t x = (f ^ c1) - c1, y = (u ^ c1) - c1, z = (v ^ c1) - c1;
+    g += x & c2;
+    q += y & c2;
+    r += z & c2;
+    c1 &= c2;                            // swap step: eta < 0 and g odd
+    eta = int32_t((uint32_t(eta) ^ c1) - 1u);
+    f += g & c1;
+    u += q & c1;
+    v += r & c1;
+    g >>= 1;
+    u <<= 1;
+    v <<= 1;
+  }
+  t[0] = int32_t(u); t[1] = int32_t(v); t[2] = int32_t(q); t[3] = int32_t(r);
+  return eta;
+}
+// (f, g) <- T (f, g) / 2^30 (exact)
+EDV_HD void update_fg(s30& f, s30& g, const int32_t t[4]) {
+  int64_t cf = int64_t(t[0]) * f.v[0] + int64_t(t[1]) * g.v[0];
+  int64_t cg = int64_t(t[2]) * f.v[0] + int64_t(t[3]) * g.v[0];
+  cf >>= 30;
+  cg >>= 30;
+#pragma unroll
+  for (int i = 1; i < 9; i++) {
+    cf += int64_t(t[0]) * f.v[i] + int64_t(t[1]) * g.v[i];
+    cg += int64_t(t[2]) * f.v[i] + int64_t(t[3]) * g.v[i];
+    f.v[i - 1] = opaque_i32(int32_t(cf) & kM30);
+    g.v[i - 1] = opaque_i32(int32_t(cg) & kM30);
+    cf >>= 30;
+    cg >>= 30;
+  }
+  f.v[8] = int32_t(cf);
+  g.v[8] = int32_t(cg);
+}
+// (d, e) <- T (d, e) / 2^30 mod p, keeping both in (-2p, p): first add the
+// multiples of p that make a negative input non-negative in effect (md, me start
+// at the matrix entries of a negative d / e), then the ones that clear the low
+// 30 bits of the numerator.
+EDV_HD void update_de(s30& d, s30& e, const int32_t t[4]) {
+  const int32_t u = t[0], v = t[1], q = t[2], r = t[3];
+  const int32_t sd = d.v[8] >> 31, se = e.v[8] >> 31;
+  int32_t md = (u & sd) + (v & se);
+  int32_t me = (q & sd) + (r & se);
+  int64_t cd = int64_t(u) * d.v[0] + int64_t(v) * e.v[0];
+  int64_t ce = int64_t(q) * d.v[0] + int64_t(r) * e.v[0];
+  md -= int32_t((kPInv30 * uint32_t(cd) + uint32_t(md)) & uint32_t(kM30));
+  me -= int32_t((kPInv30 * uint32_t(ce) + uint32_t(me)) & uint32_t(kM30));
+  cd += int64_t(-19) * md;
+  ce += int64_t(-19) * me;
+  cd >>= 30;
+  ce >>= 30;
+#pragma unroll
+  for (int i = 1; i < 9; i++) {
+    cd += int64_t(u) * d.v[i] + int64_t(v) * e.v[i];
+    ce += int64_t(q) * d.v[i] + int64_t(r) * e.v[i];
+    if (i == 8) {
+      cd += int64_t(32768) * md;
+      ce += int64_t(32768) * me;
+    }
+    d.v[i - 1] = opaque_i32(int32_t(cd) & kM30);
+    e.v[i - 1] = opaque_i32(int32_t(ce) & kM30);
+    cd >>= 30;
+    ce >>= 30;
+  }
+  d.v[8] = int32_t(cd);
+  e.v[8] = int32_t(ce);
+}
+EDV_HD fe fe_invert_safegcd(const fe& z) {
+  uint32_t w[8];
+  fe_tobytes(w, z);  // canonical 0 <= z < p
+  s30 f, g, d, e;
+  g.v[0] = int32_t(w[0] & kM30);
+#pragma unroll
+  for (int i = 1; i < 8; i++) {
+    const int pos = 30 * i, wi = pos >> 5, sh = pos & 31;
+    g.v[i] = int32_t(((w[wi] >> sh) | (sh ? (w[wi + 1] << (32 - sh)) : 0u)) & uint32_t(kM30));
+  }
+  g.v[8] = int32_t(w[7] >> 16);  // bits 240..255
+#pragma unroll
+  for (int i = 0; i < 9; i++) g.v[i] = opaque_i32(g.v[i]);
+#pragma unroll
+  for (int i = 0; i < 9; i++) { f.v[i] = 0; d.v[i] = 0; e.v[i] = 0; }
+  f.v[0] = -19;
+  f.v[8] = 32768;
+  e.v[0] = 1;
+  int32_t eta = -1;
+#pragma unroll 1
+  for (int it = 0; it < 20; it++) {
+    int32_t t[4];
+    eta = divsteps_30(eta, uint32_t(f.v[0]), uint32_t(g.v[0]), t);
+    update_de(d, e, t);
+    update_fg(f, g, t);
+  }
+  // f = +-1: z^-1 = sign(f) * d (mod p); d (|d| < 2p) regrouped into the
+  // radix-2^25.5 columns, then carried (bits above 2^255 fold in with 19)
+  const int64_t sgn = (f.v[8] >> 31) | 1;  // f.v[8] is 0 or -1 when f = +-1
+  constexpr int kPos[10] = {0, 26, 51, 77, 102, 128, 153, 179, 204, 230};
+  int64_t h[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int pos = 30 * i;
+    int k = 0;  // the radix-2^25.5 limb whose range holds bit 30 i
+#pragma unroll
+    for (int j = 0; j < 10; j++)
+      if (kPos[j] <= pos) k = j;
+    h[k] += (sgn * int64_t(d.v[i])) * (int64_t(1) << (pos - kPos[k]));
+  }
+  return fe_carry64(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
+}
+
 // ---------------------------------------------------------------- the group
 struct ge_p2 { fe X, Y, Z; };
 struct ge_p3 { fe X, Y, Z, T; };
@@ -438,7 +580,7 @@ EDV_HD bool ge_frombytes_negate(ge_p3& h, const uint32_t s[8]) {
 }
 
 EDV_HD void ge_p2_tobytes(uint32_t w[8], const ge_p2& p) {
-  const fe zi = fe_invert(p.Z);
+  const fe zi = fe_invert_safegcd(p.Z);
   const fe x = fe_mul(p.X, zi);
   const fe y = fe_mul(p.Y, zi);
   fe_tobytes(w, y);

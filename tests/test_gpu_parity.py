@@ -246,3 +246,20 @@ def test_request_digests_and_state_keys():
     assert digest.request_digests(reqs) == want
     nyms = [c["msg"]["identifier"] for c in cases] + ["", "V4SGRU86Z58d6TV7PBUe6f"]
     assert digest.nym_state_keys(nyms) == [hashlib.sha256(n.encode()).digest() for n in nyms]
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_length_bucket_modes_same_verdicts(mode):
+    """edv_set_length_buckets never changes verdicts (device path, ragged batch)."""
+    sigs, pks, msgs, off = orc.corpus(0xB0C + mode, 0, 3000, mode=1, invalid_permille=120)
+    want = checker(sigs, pks, msgs, off)
+    bufs = [edv.DeviceBuffer(a.nbytes + 64) for a in (sigs, pks, msgs, off)]
+    for b, a in zip(bufs, (sigs, pks, msgs, off)):
+        b.upload(a)
+    acc = edv.DeviceBuffer(3000)
+    try:
+        edv.set_length_buckets(0, mode)
+        edv.verify_device(bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, 3000, acc.ptr)
+        assert np.array_equal(acc.download(3000), want)
+    finally:
+        edv.set_length_buckets(0, 2)

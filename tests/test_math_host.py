@@ -82,6 +82,26 @@ def test_fe_invert_and_pow22523():
         assert val(h) % P == pow(x, (P - 5) // 8, P)
 
 
+def test_fe_invert_safegcd():
+    """The divsteps inversion the encode uses (V9) against pow(x, p - 2, p), on
+    canonical, non-canonical and bound-extreme limb vectors."""
+    hc = hostcheck_lib.load()
+    r = random.Random(17)
+    h = (ctypes.c_int32 * 10)()
+    xs = [1, 2, 3, 19, P - 1, P - 2, (P - 1) // 2, 2**254, 2**255 - 20] + [r.randrange(1, P) for _ in range(3000)]
+    for x in xs:
+        hc.hc_fe_invert_safegcd(arr(limbs(x)), h)
+        assert val(h) % P == pow(x, P - 2, P) and out_ok(h), x
+    for it in range(3000):  # arbitrary (non-canonical, signed) limb vectors within the mul input bounds
+        f = rand_limbs(r, extreme=(it % 2 == 0))
+        if val(f) % P == 0:
+            continue
+        hc.hc_fe_invert_safegcd(arr(f), h)
+        assert val(h) % P == pow(val(f) % P, P - 2, P) and out_ok(h)
+    hc.hc_fe_invert_safegcd(arr([0] * 10), h)
+    assert val(h) % P == 0
+
+
 def test_sc_reduce_canonical():
     hc = hostcheck_lib.load()
     r = random.Random(8)
