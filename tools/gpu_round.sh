@@ -32,7 +32,7 @@ export TMPDIR=/tmp
 if has prof; then
   log rocprof
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- \
-    python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/prof_bench.log 2>&1 || { tail -30 $O/prof_bench.log; exit 1; }
+    python3 $R/bench.py --no-cpu-baseline > $O/prof_bench.log 2>&1 || { tail -30 $O/prof_bench.log; exit 1; }
   find $O/prof -name "*stats*"
 fi
 if has pmc; then
@@ -41,7 +41,7 @@ if has pmc; then
     i=$((i+1))
     log "pmc $C"
     timeout -k 10 -s KILL 240 rocprofv3 --pmc $C -d $O/pmc$i -o run --output-format csv -- \
-      python3 $R/bench.py --steps 6 --warmup 1 --no-cpu-baseline > $O/pmc$i.log 2>&1 || { echo "pmc $C failed"; tail -20 $O/pmc$i.log; exit 1; }
+      python3 $R/bench.py --steps 6 --warmup 20 --no-cpu-baseline > $O/pmc$i.log 2>&1 || { echo "pmc $C failed"; tail -20 $O/pmc$i.log; exit 1; }
   done
 fi
 log done
