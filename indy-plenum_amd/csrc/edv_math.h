@@ -125,15 +125,20 @@ EDV_HD int32_t carry_biased(int64_t t, int64_t& next) {
 // is unbiased, so its second step is an ordinary carry_step.
 EDV_HD fe fe_carry64_biased(int64_t h0, int64_t h1, int64_t h2, int64_t h3, int64_t h4, int64_t h5, int64_t h6,
                             int64_t h7, int64_t h8, int64_t h9) {
+  // One sequential pass 0 -> 9, the 2^255 = 19 fold, then 0 -> 1: eleven steps
+  // (ten of them on biased columns) against twelve for ref10's two interleaved
+  // chains, which need h4 carried twice.  Every column is carried once before it
+  // is read as a limb, so the output bounds are those of fe_carry64: a column
+  // is < 2^62, its carry < 2^37 adds into the next 64-bit column, 19 * c9 < 2^42
+  // lands on the reduced h0 and h0's last carry (< 2^17) on the reduced h1.
   h0 = carry_biased<26>(h0, h1);
-  h4 = carry_biased<26>(h4, h5);
   h1 = carry_biased<25>(h1, h2);
-  h5 = carry_biased<25>(h5, h6);
   h2 = carry_biased<26>(h2, h3);
-  h6 = carry_biased<26>(h6, h7);
   h3 = carry_biased<25>(h3, h4);
+  h4 = carry_biased<26>(h4, h5);
+  h5 = carry_biased<25>(h5, h6);
+  h6 = carry_biased<26>(h6, h7);
   h7 = carry_biased<25>(h7, h8);
-  h4 = carry_step<26>(h4, h5);
   h8 = carry_biased<26>(h8, h9);
   int64_t c9 = 0;
   h9 = carry_biased<25>(h9, c9);
@@ -163,6 +168,7 @@ EDV_HD fe fe_mul(const fe& f, const fe& g) {
     g19[i] = 19 * g.v[i];
     f2[i] = (i & 1) ? 2 * f.v[i] : f.v[i];
   }
+  const int32_t f38_9 = 38 * f.v[9];
   int64_t h[10];
 #pragma unroll
   for (int k = 0; k < 10; k++) {
@@ -170,8 +176,11 @@ EDV_HD fe fe_mul(const fe& f, const fe& g) {
 #pragma unroll
     for (int i = 0; i < 10; i++) {
       const int j = k - i;
-      const int32_t a = ((k & 1) == 0) ? f2[i] : f.v[i];
-      const int32_t b = (j >= 0) ? g.v[j] : g19[j + 10];
+      // f_9 g_j with j odd wraps with weight 2 * 19: as (38 f_9) g_j, so
+      // neither 2 f_9 nor 19 g_1 is needed (13 premultiplied operands, not 14)
+      const bool f9w = (i == 9) && (j < 0) && ((j + 10) & 1);
+      const int32_t a = f9w ? f38_9 : ((k & 1) == 0) ? f2[i] : f.v[i];
+      const int32_t b = f9w ? g.v[j + 10] : (j >= 0) ? g.v[j] : g19[j + 10];
       acc = (i == 0) ? int64_t(a) * int64_t(b) + bias_reg(k) : acc + int64_t(a) * int64_t(b);
     }
     h[k] = acc;
@@ -181,10 +190,40 @@ EDV_HD fe fe_mul(const fe& f, const fe& g) {
   return r;
 }
 
-// Squaring columns (55 products): term f_i f_j (i <= j) with multiplier
+// Squaring columns (55 products): term f_i f_j (i <= j) carries the constant
 // (i<j ? 2 : 1) * (i,j both odd ? 2 : 1) * (i+j >= 10 ? 19 : 1) (* 2 for
-// DOUBLE, i.e. 2 f^2), split between the two operands so each stays inside
-// int32 under the mul input bounds.  Columns start at col_bias.
+// DOUBLE, i.e. 2 f^2), applied as (x f_i) * (y f_j) with x y = that constant.
+// The split {x, y} below keeps each premultiplied operand inside int32 under
+// the mul input bounds (x <= 19 on even limbs, <= 38 on odd limbs) and uses the
+// fewest distinct premultiplied operands, one instruction each: 13 for f^2 and
+// 21 for 2 f^2 (tools/derive_sq_split.py, a small 0/1 ILP; the earlier hand
+// rule needed 17 and 27).  Columns start at col_bias.
+struct sq_split { int8_t x, y; };
+constexpr sq_split kSqSplit[2][10][10] = {
+    {
+        {{1, 1}, {1, 2}, {1, 2}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}},
+        {{0, 0}, {1, 2}, {2, 1}, {2, 2}, {2, 1}, {2, 2}, {1, 2}, {2, 2}, {2, 1}, {2, 38}},
+        {{0, 0}, {0, 0}, {1, 1}, {1, 2}, {2, 1}, {1, 2}, {1, 2}, {1, 2}, {2, 19}, {1, 38}},
+        {{0, 0}, {0, 0}, {0, 0}, {1, 2}, {2, 1}, {2, 2}, {2, 1}, {2, 38}, {2, 19}, {2, 38}},
+        {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {1, 1}, {1, 2}, {2, 19}, {1, 38}, {2, 19}, {1, 38}},
+        {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {19, 2}, {2, 19}, {2, 38}, {2, 19}, {2, 38}},
+        {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {19, 1}, {1, 38}, {2, 19}, {1, 38}},
+        {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {1, 38}, {2, 19}, {2, 38}},
+        {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {1, 19}, {1, 38}},
+        {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {1, 38}},
+    },
+    {
+        {{1, 2}, {1, 4}, {2, 2}, {1, 4}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {1, 4}},
+        {{0, 0}, {4, 1}, {4, 1}, {8, 1}, {4, 1}, {8, 1}, {1, 4}, {4, 2}, {4, 1}, {8, 19}},
+        {{0, 0}, {0, 0}, {2, 1}, {1, 4}, {2, 2}, {4, 1}, {2, 2}, {4, 1}, {4, 19}, {4, 19}},
+        {{0, 0}, {0, 0}, {0, 0}, {1, 4}, {1, 4}, {4, 2}, {1, 4}, {4, 38}, {4, 19}, {4, 38}},
+        {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {1, 2}, {4, 1}, {4, 19}, {2, 38}, {4, 19}, {4, 19}},
+        {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {38, 2}, {38, 2}, {4, 38}, {4, 19}, {38, 4}},
+        {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {2, 19}, {2, 38}, {4, 19}, {19, 4}},
+        {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {38, 2}, {38, 2}, {38, 4}},
+        {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {2, 19}, {19, 4}},
+        {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {19, 4}},
+    }};
 template <bool DOUBLE>
 EDV_HD void fe_sq_cols(const fe& f, int64_t h[10]) {
   bool first[10];
@@ -195,29 +234,8 @@ EDV_HD void fe_sq_cols(const fe& f, int64_t h[10]) {
 #pragma unroll
     for (int j = i; j < 10; j++) {
       const int k = (i + j) % 10;
-      const bool wrap = (i + j) >= 10;
-      const bool oo = (i & 1) && (j & 1);
-      int32_t a = f.v[i], b = f.v[j];
-      // distribute the constant factor: 2 (i<j), 2 (odd-odd), 19 (wrap)
-      int ma = 1, mb = 1;
-      if (i < j) ma *= 2;
-      if (oo) mb *= 2;
-      if (wrap) {
-        // 19 goes on an operand that can hold it: odd limbs (<=1.65*2^25) take 38 at most,
-        // even limbs (<=1.65*2^26) take 19 at most (and 2 on the other operand).
-        if ((j & 1) && mb == 1) mb = 19;        // i even, j odd: 2 on f_i, 19 on f_j
-        else if ((j & 1) && mb == 2) mb = 38;   // both odd: (2 on f_i), 38 on f_j
-        else if (ma == 1) ma = 19;              // i == j even: 19
-        else if (i & 1) ma = 38;                // i odd, j even: 38 on f_i
-        else mb = 19;                           // both even, i < j: 2 on f_i, 19 on f_j
-      }
-      // the extra 2 of 2 f^2 goes on the operand without the 19 (at most 4 f_i then)
-      if (DOUBLE) {
-        if (ma <= 2) ma *= 2;
-        else mb *= 2;
-      }
-      a = a * ma;
-      b = b * mb;
+      const sq_split m = kSqSplit[DOUBLE ? 1 : 0][i][j];
+      const int32_t a = f.v[i] * int32_t(m.x), b = f.v[j] * int32_t(m.y);
       h[k] = first[k] ? int64_t(a) * int64_t(b) + bias_reg(k) : h[k] + int64_t(a) * int64_t(b);
       first[k] = false;
     }
