@@ -37,7 +37,7 @@ def main():
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py",
            "correction": "read_bytes = 2 * FETCH_SIZE_KB * 1024 (gfx950), write_bytes = WRITE_SIZE_KB * 1024",
            "kernel_source_sha256": kernel_source_hash(),
-           "bench_args": "--steps 6 --warmup 1 --no-cpu-baseline (batch 65536 x 256 B)",
+           "bench_args": "--steps 6 --warmup 20 --no-cpu-baseline (batch 65536 x 256 B)",
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f, nf = fetch.get(k, (0.0, 0))
