@@ -26,11 +26,11 @@ struct HostBTab {
 };
 struct HostComb {
   std::vector<int32_t> w;
-  HostComb() : w(kCombRows * kBEntries * kBStride) {
+  HostComb() : w(kCombRows * kCombEntries * kBStride) {
     for (int i = 0; i < kCombRows; i++)
-      for (int j = 0; j < kBEntries; j++) comb_entry(w.data() + (i * kBEntries + j) * kBStride, i, j);
+      for (int j = 0; j < kCombEntries; j++) comb_entry(w.data() + (i * kCombEntries + j) * kBStride, i, j);
   }
-  ge_precomp entry(int i, int j) const { return precomp_from_words(w.data() + (i * kBEntries + j) * kBStride); }
+  ge_precomp entry(int i, int j) const { return precomp_from_words(w.data() + (i * kCombEntries + j) * kBStride); }
 };
 const HostComb& comb() {
   static HostComb c;

@@ -97,18 +97,20 @@ struct GlobalATab {
     return c;
   }
 };
-// Shared B table in LDS, read as 16-byte vectors.
-struct LdsBTab {
-  const int32_t* lds;
+// Shared 0..2^15 x B table in global memory (4 MiB, L2/MALL-resident), read as
+// 16-byte vectors: too large for LDS, and each lane touches one 128-byte entry
+// every fourth window.
+struct GlobalBTab {
+  const int32_t* w;
   __device__ __forceinline__ ge_precomp entry(int j) const {
-    const int4* p = reinterpret_cast<const int4*>(lds + j * kBStride);
-    int32_t w[32];
+    const int4* p = reinterpret_cast<const int4*>(w + j * kBStride);
+    int32_t t[32];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int4 v = p[i];
-      w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+      t[4 * i] = v.x; t[4 * i + 1] = v.y; t[4 * i + 2] = v.z; t[4 * i + 3] = v.w;
     }
-    return precomp_from_words(w);
+    return precomp_from_words(t);
   }
 };
 
@@ -148,10 +150,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 8))) 
 
 // Phase 2: V8 double-scalar multiplication and V9 compare (~85% of the work).
 __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
-  __shared__ __attribute__((aligned(16))) int32_t btab[kBEntries * kBStride];
-  for (int t = threadIdx.x; t < kBEntries * kBStride / 4; t += kBlock)
-    reinterpret_cast<int4*>(btab)[t] = reinterpret_cast<const int4*>(a.btab)[t];
-  __syncthreads();
   const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= a.n || !a.st.alive[j]) return;
   const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
@@ -163,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
     sd[k] = a.st.dig[uint64_t(8 + k) * a.st.cap + j];
   }
   const GlobalATab at{a.st.atab + j * kAWords};
-  const LdsBTab bt{btab};
+  const GlobalBTab bt{a.btab};
   a.accept[i] = main_one(R, hd, sd, at, bt) ? 1 : 0;
 }
 
@@ -171,7 +169,7 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
 struct GlobalComb {
   const int32_t* w;
   __device__ __forceinline__ ge_precomp entry(int i, int j) const {
-    const int4* p = reinterpret_cast<const int4*>(w + (i * kBEntries + j) * kBStride);
+    const int4* p = reinterpret_cast<const int4*>(w + (i * kCombEntries + j) * kBStride);
     int32_t t[32];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
@@ -202,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void edv_sign_kernel(const uint32_t* seeds,
 
 __global__ void edv_comb_kernel(int32_t* out) {
   const int t = threadIdx.x + blockIdx.x * blockDim.x;
-  if (t < kCombRows * kBEntries) comb_entry(out + t * kBStride, t / kBEntries, t % kBEntries);
+  if (t < kCombRows * kCombEntries) comb_entry(out + t * kBStride, t / kCombEntries, t % kCombEntries);
 }
 
 // ---- length buckets (config C4): group the chunk's requests by SHA-512 block
@@ -261,7 +259,7 @@ __global__ __launch_bounds__(kBlock) void edv_bucket_scatter_kernel(const uint64
   if (j < n) perm[wbase[b] + rank] = uint32_t(j);
 }
 
-// j * B for j = 0..128 in affine precomp form, once per device
+// j * B for j = 0..2^15 in affine precomp form, once per device
 __global__ void edv_btab_kernel(int32_t* out) {
   const int j = threadIdx.x + blockIdx.x * blockDim.x;
   if (j < kBEntries) btab_entry(out + j * kBStride, j);
@@ -721,8 +719,8 @@ int edv_time_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_
 
 static int ensure_comb(DevCtx& c) {
   if (c.comb) return 0;
-  HIPOK(hipMalloc(&c.comb, uint64_t(kCombRows) * kBEntries * kBStride * 4), "hipMalloc comb");
-  const int total = kCombRows * kBEntries;
+  HIPOK(hipMalloc(&c.comb, uint64_t(kCombRows) * kCombEntries * kBStride * 4), "hipMalloc comb");
+  const int total = kCombRows * kCombEntries;
   edv_comb_kernel<<<(total + 63) / 64, 64, 0, c.stream>>>(c.comb);
   HIPOK(hipGetLastError(), "comb launch");
   HIPOK(hipStreamSynchronize(c.stream), "comb sync");

@@ -12,8 +12,10 @@
 namespace edv {
 
 constexpr int kAEntries = 9;   // per-lane table 0..8 x (-A), cached form (entry 0 = identity)
-constexpr int kBEntries = 129; // shared table 0..128 x B, affine precomp form
-constexpr int kBStride = 32;   // words per B entry (30 used; 128-byte aligned)
+constexpr int kBBits = 16;                     // radix 2^16 digits of S
+constexpr int kBEntries = (1 << (kBBits - 1)) + 1; // shared table 0..2^15 x B, affine precomp form (4 MiB)
+constexpr int kCombEntries = 129;               // signer comb rows: 0..128 x 256^i B
+constexpr int kBStride = 32;                    // words per B / comb entry (30 used; 128-byte aligned)
 
 // ------------------------------------------------------------- message words
 EDV_HD uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
@@ -100,8 +102,8 @@ EDV_HD void recode4(uint32_t out[8], const uint32_t h[8]) {
     out[w] = packed;
   }
 }
-// S: 32 signed radix-256 digits in [-128, 127] (S < 2^253 keeps the top digit
-// <= 32; larger S is rejected by V2 and only has to stay in table bounds).
+// S (signer scalars): 32 signed radix-256 digits in [-128, 127] (k < 2^253 keeps
+// the top digit <= 32).
 EDV_HD void recode8(uint32_t out[8], const uint32_t s[8]) {
   int carry = 0;
 #pragma unroll
@@ -113,6 +115,24 @@ EDV_HD void recode8(uint32_t out[8], const uint32_t s[8]) {
       carry = (w == 7 && k == 3) ? 0 : ((e + 128) >> 8);
       e -= carry * 256;
       packed |= uint32_t(e & 255) << (8 * k);
+    }
+    out[w] = packed;
+  }
+}
+// S (verify, V8): 16 signed radix-2^16 digits in [-2^15, 2^15), packed as 16-bit
+// two's complement, digit k at bits 16*(k%2) of word k/2.  V2 leaves S < 2^253,
+// so the top digit is <= 2^13 + 1 and stays inside the 0..2^15 table.
+EDV_HD void recode16(uint32_t out[8], const uint32_t s[8]) {
+  int carry = 0;
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      int e = int((s[w] >> (16 * k)) & 0xffff) + carry;
+      carry = (w == 7 && k == 1) ? 0 : ((e + 0x8000) >> 16);
+      e -= carry * 0x10000;
+      packed |= uint32_t(e & 0xffff) << (16 * k);
     }
     out[w] = packed;
   }
@@ -132,7 +152,7 @@ EDV_HD ge_precomp precomp_from_words(const int32_t* w) {
   return q;
 }
 
-// j * B for j in [0, 128], affine precomp form, written as kBStride words.
+// j * B for j in [0, 2^15], affine precomp form, written as kBStride words.
 EDV_HD void btab_entry(int32_t* o, int j) {
   const uint32_t Bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                           0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
@@ -141,7 +161,7 @@ EDV_HD void btab_entry(int32_t* o, int j) {
   const ge_p3 B{fe_neg(nB.X), nB.Y, nB.Z, fe_neg(nB.T)};
   const ge_cached Bc = ge_p3_to_cached(B);
   ge_p3 acc = ge_p3_identity();
-  for (int bit = 7; bit >= 0; bit--) {
+  for (int bit = kBBits - 1; bit >= 0; bit--) {
     acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
     if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add(acc, Bc));
   }
@@ -171,7 +191,7 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
   hram(dig, R, A, m, mlen);
   sc_reduce(h, dig);
   recode4(hd, h);
-  recode8(sd, S);
+  recode16(sd, S);
   const ge_cached c1 = ge_p3_to_cached(nA);
   at.store(0, ge_cached_identity());
   at.store(1, c1);
@@ -187,7 +207,8 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
 
 // Phase 2 (kernel edv_main_kernel): V8 R' = [h](-A) + [S]B by a joint
 // fixed-window walk, top digit first -- every lane adds at the same positions,
-// so a wave never diverges -- then V9 encode(R') == R.  ATab provides load(e);
+// so a wave never diverges -- then V9 encode(R') == R.  [S]B adds one radix-2^16
+// digit every fourth window (16 mixed additions instead of 32 at radix 256).  ATab provides load(e);
 // BTab provides entry(j) -> precomp.
 template <class ATab, class BTab>
 EDV_HD bool main_one(const uint32_t R[8], uint32_t hd[8], uint32_t sd[8], const ATab& at, const BTab& bt) {
@@ -200,9 +221,9 @@ EDV_HD bool main_one(const uint32_t R[8], uint32_t hd[8], uint32_t sd[8], const 
     ge_cached c = at.load(dA < 0 ? -dA : dA);
     int dB = 0;
     ge_precomp q;
-    if ((w & 1) == 0) {
-      dB = int32_t(sd[7]) >> 24;
-      shl256<8>(sd);
+    if ((w & 3) == 0) {
+      dB = int32_t(sd[7]) >> 16;
+      shl256<16>(sd);
       q = bt.entry(dB < 0 ? -dB : dB);
     }
     ge_p3 p3;
@@ -216,7 +237,7 @@ EDV_HD bool main_one(const uint32_t R[8], uint32_t hd[8], uint32_t sd[8], const 
     }
     c = ge_cached_cneg(c, dA < 0);
     ge_p1p1 t = ge_add(p3, c);
-    if ((w & 1) == 0) {
+    if ((w & 3) == 0) {
       p3 = ge_p1p1_to_p3(t);
       t = ge_madd(p3, ge_precomp_cneg(q, dB < 0));
     }
