@@ -95,6 +95,17 @@ void hc_sha256(const uint8_t* m, uint64_t mlen, int misalign, uint8_t* out32) {
   store_words(out32, o, 8);
 }
 void hc_btab(int32_t* out) { memcpy(out, btab().w.data(), sizeof(int32_t) * kBEntries * kBStride); }
+int hc_btab_entries() { return kBEntries; }
+// packed signed digits of a 32-byte scalar: radix 4 -> recode4 (h), 8 -> recode8 (signer), 16 -> recode16 (S)
+int hc_recode(const uint8_t* in32, int bits, uint32_t* out8) {
+  uint32_t w[8];
+  load_words(w, in32, 8);
+  if (bits == 4) recode4(out8, w);
+  else if (bits == 8) recode8(out8, w);
+  else if (bits == 16) recode16(out8, w);
+  else return -1;
+  return 0;
+}
 int hc_sign_batch(const uint8_t* seeds, const uint8_t* msgs, const uint64_t* off, uint64_t n, uint8_t* pks,
                   uint8_t* sigs) {
   const HostComb& ct = comb();

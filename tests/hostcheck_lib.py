@@ -20,5 +20,7 @@ def load():
         _lib = ctypes.CDLL(SO)
         _lib.hc_hram.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
         _lib.hc_sha256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+        _lib.hc_recode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p]
+        _lib.hc_btab.argtypes = [ctypes.c_void_p]
         _lib.hc_verify_batch.argtypes = [ctypes.c_char_p] * 3 + [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
     return _lib

@@ -149,3 +149,53 @@ def test_kernel_algorithm_on_cpu_matches_libsodium_golden(golden, golden_meta):
     cats = golden_meta["categories"]
     bad = [(i, cats[g[1]]) for i, g in enumerate(golden) if acc.raw[i] != g[0]]
     assert bad == []
+
+
+def _digits(packed, bits):
+    per = 32 // bits
+    out = []
+    for k in range(256 // bits):
+        raw = (packed[k // per] >> (bits * (k % per))) & ((1 << bits) - 1)
+        out.append(raw - (1 << bits) if raw >> (bits - 1) else raw)
+    return out
+
+
+def test_scalar_recoding_radix_4_8_16():
+    """Signed digits the main loop consumes: h (radix 16, digit in [-8, 7]),
+    S (radix 2^16, |d| <= 2^15 so it indexes the 0..2^15 B table) and signer
+    scalars (radix 256); sum d_k * 2^(bits*k) must give back the scalar."""
+    hc = hostcheck_lib.load()
+    r = random.Random(12)
+    out = (ctypes.c_uint32 * 8)()
+    # V2 admits every S < 2^252 and canonical S < L; h and signer scalars are < L
+    edge = [0, 1, L - 1, 2**252 - 1, 2**252, 2**253 - 1 - (2**253 - L)]
+    edge += [int("8000" * 16, 16) % L, int("7fff" * 16, 16) % L, int("ffff" * 15, 16), int("80" * 31, 16)]
+    edge += [int("88" * 31, 16), int("77" * 31, 16)]
+    vals = [v for v in edge if 0 <= v < L] + [r.randrange(L) for _ in range(2000)]
+    for bits, lo, hi in ((4, -8, 7), (8, -128, 127), (16, -2**15, 2**15)):
+        for v in vals:
+            assert hc.hc_recode(v.to_bytes(32, "little"), bits, out) == 0
+            d = _digits(list(out), bits)
+            assert sum(x << (bits * k) for k, x in enumerate(d)) == v, (bits, hex(v))
+            assert all(lo <= x <= hi for x in d[:-1]), (bits, hex(v))
+            assert 0 <= d[-1] <= hi, (bits, hex(v))
+
+
+def test_btab_entries_are_multiples_of_B():
+    """The 0..2^15 x B table (affine y+x, y-x, 2dxy limbs) against the oracle's [j]B."""
+    import oracle_lib as orc
+    hc = hostcheck_lib.load()
+    n = hc.hc_btab_entries()
+    assert n == 2**15 + 1
+    tab = (ctypes.c_int32 * (n * 32))()
+    hc.hc_btab(tab)
+    d = (-121665 * pow(121666, P - 2, P)) % P
+    r = random.Random(13)
+    for j in [0, 1, 2, 3, 127, 128, 129, 255, 256, 4097, 32767, 32768] + [r.randrange(n) for _ in range(40)]:
+        e = list(tab[32 * j: 32 * j + 32])
+        ypx, ymx, xy2d = val(e[0:10]) % P, val(e[10:20]) % P, val(e[20:30]) % P
+        inv2 = pow(2, P - 2, P)
+        y, x = (ypx + ymx) * inv2 % P, (ypx - ymx) * inv2 % P
+        assert xy2d == 2 * d * x * y % P, j
+        enc = int.to_bytes(y | ((x & 1) << 255), 32, "little")
+        assert enc == orc.scalarmult_base(j.to_bytes(32, "little")), j
