@@ -565,12 +565,34 @@ EDV_HD ge_p1p1 ge_madd(const ge_p3& p, const ge_precomp& q) {
   r.T = fe_sub(D, C);
   return r;
 }
-EDV_HD ge_cached ge_cached_cneg(const ge_cached& c, bool neg) {
-  return ge_cached{fe_select(c.YpX, c.YmX, neg), fe_select(c.YmX, c.YpX, neg), c.Z,
-                   fe_select(c.T2d, fe_neg(c.T2d), neg)};
+// Conditional negation by an all-ones/zero lane mask in plain VOP2 logic (xor
+// swap, (t ^ m) - m): the mask is opaque, so LLVM cannot turn it back into the
+// 60 v_cndmask_b32 per window a select-based version compiles to.
+EDV_HD void fe_cswap_mask(fe& a, fe& b, int32_t m) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const int32_t t = (a.v[i] ^ b.v[i]) & m;
+    a.v[i] ^= t;
+    b.v[i] ^= t;
+  }
 }
-EDV_HD ge_precomp ge_precomp_cneg(const ge_precomp& c, bool neg) {
-  return ge_precomp{fe_select(c.ypx, c.ymx, neg), fe_select(c.ymx, c.ypx, neg), fe_select(c.xy2d, fe_neg(c.xy2d), neg)};
+EDV_HD fe fe_cneg_mask(const fe& a, int32_t m) {
+  fe h;
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = (a.v[i] ^ m) - m;
+  return h;
+}
+EDV_HD ge_cached ge_cached_cneg(ge_cached c, bool neg) {
+  const int32_t m = opaque_i32(-int32_t(neg));
+  fe_cswap_mask(c.YpX, c.YmX, m);
+  c.T2d = fe_cneg_mask(c.T2d, m);
+  return c;
+}
+EDV_HD ge_precomp ge_precomp_cneg(ge_precomp c, bool neg) {
+  const int32_t m = opaque_i32(-int32_t(neg));
+  fe_cswap_mask(c.ypx, c.ymx, m);
+  c.xy2d = fe_cneg_mask(c.xy2d, m);
+  return c;
 }
 
 // libsodium ge25519_frombytes_negate_vartime: decode, return -P.  false = not on curve.
