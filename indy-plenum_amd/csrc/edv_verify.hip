@@ -10,8 +10,9 @@
 //   V8     R' = [h](-A) + [S]B with FIXED windows so all 64 lanes of a wave
 //          stay in lock-step: h in 64 signed 4-bit digits against a per-lane
 //          table 1..8 x (-A) (cached form, in a coalesced global scratch
-//          buffer), S in 32 signed 8-bit digits against a shared 129-entry
-//          affine table of j*B held in LDS; 252 doublings, 64 + 32 additions
+//          buffer), S in 16 signed 16-bit digits against a shared
+//          0..2^15 affine table of j*B (4 MiB, global memory, L2/MALL);
+//          252 doublings, 64 + 16 additions
 //   V9     encode R' (one inversion) and compare its 32 bytes with R
 // No MFMA: this is scalar bignum integer work (v_mad_i64_i32 chains).
 #include <hip/hip_runtime.h>
@@ -39,7 +40,7 @@ constexpr uint64_t kChunkDefault = uint64_t(1) << 18;  // signatures per prep/ma
 // Per-chunk state handed from the prep kernel to the main kernel, SoA so every
 // wave-wide load/store touches 64 consecutive words:
 //   atab[360 * i + w]  word w (0..359) of signature i's 0..8 x (-A) table
-//   dig[w * cap + i]   w 0..7: packed radix-16 digits of h, 8..15: radix-256 digits of S
+//   dig[w * cap + i]   w 0..7: packed radix-16 digits of h, 8..15: radix-2^16 digits of S
 //   alive[i]           1 if V2-V5 passed (the main kernel skips dead lanes' work)
 struct ChunkState {
   int32_t* atab;
