@@ -15,11 +15,12 @@
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
 
-enum Op { ADD, MAD64, MULLO, MULHI, MAD24, MULHI24, FMA64, ADDC, DOT2, ALIGNBIT, ADD3, LSHLADD64, FMA32, BFI, XOR, CNDMASK, ADDCO3, MADMIX, LSHR };
+enum Op { ADD, MAD64, MULLO, MULHI, MAD24, MULHI24, FMA64, ADDC, DOT2, ALIGNBIT, ADD3, LSHLADD64, FMA32, BFI, XOR, CNDMASK, ADDCO3, MADMIX, LSHR, ASHR64, MADI64, BITOP3, CND64, MULI24 };
 static const char* kNames[] = {"v_add_u32", "v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32",
   "v_mad_u32_u24", "v_mul_hi_u32_u24", "v_fma_f64", "v_add_co+v_addc_co (2 instr)",
-  "v_dot2_u32_u16", "v_alignbit_b32", "v_add3_u32", "v_lshl_add_u64", "v_fma_f32", "v_bfi_b32", "v_xor_b32", "v_cndmask_b32", "v_add_co_u32(vop3 sdst)", "v_mad_u64_u32+v_add_u32 (2 instr)", "v_lshrrev_b32"};
-static const int kInstrPerStep[] = {1,1,1,1,1,1,1,2,1,1,1,1,1,1,1,1,1,2,1};
+  "v_dot2_u32_u16", "v_alignbit_b32", "v_add3_u32", "v_lshl_add_u64", "v_fma_f32", "v_bfi_b32", "v_xor_b32", "v_cndmask_b32", "v_add_co_u32(vop3 sdst)", "v_mad_u64_u32+v_add_u32 (2 instr)", "v_lshrrev_b32",
+  "v_ashrrev_i64", "v_mad_i64_i32", "v_bitop3_b32", "v_cndmask_b32_e64 (sgpr mask)", "v_mul_i32_i24"};
+static const int kInstrPerStep[] = {1,1,1,1,1,1,1,2,1,1,1,1,1,1,1,1,1,2,1,1,1,1,1,1};
 
 constexpr int ITERS = 4096;   // loop trips
 constexpr int UNR = 8;       // chains per lane (independent)
@@ -35,6 +36,7 @@ __global__ __launch_bounds__(256) void kbench(uint32_t* out, uint32_t seed) {
   for (int i = 0; i < UNR; i++) { r[i] = x + i; q[i] = ((uint64_t)y << 32) | (x + i); d[i] = (double)(x + i); f[i] = (float)(x + i); }
   double dx = (double)x * 1e-9, dy = (double)y * 1e-9;
   float fx = (float)x * 1e-9f, fy = (float)y * 1e-9f;
+  const uint64_t mask = __builtin_amdgcn_read_exec() & 0x5555555555555555ull;
   for (int it = 0; it < ITERS; it++) {
 #pragma unroll
     for (int rep = 0; rep < 4; rep++) {
@@ -59,6 +61,11 @@ __global__ __launch_bounds__(256) void kbench(uint32_t* out, uint32_t seed) {
         if constexpr (OP == ADDCO3) asm volatile("v_add_co_u32 %0, s[0:1], %0, %1" : "+v"(r[i]) : "v"(x) : "s0", "s1");
         if constexpr (OP == MADMIX) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0\n\tv_add_u32 %3, %3, %1" : "+v"(q[i]), "+v"(r[i]) : "v"(x), "v"(y) : "vcc");
         if constexpr (OP == LSHR) asm volatile("v_lshrrev_b32 %0, 7, %0" : "+v"(r[i]));
+        if constexpr (OP == ASHR64) asm volatile("v_ashrrev_i64 %0, 26, %1" : "=v"(q[i]) : "v"(q[(i + 1) % UNR]));
+        if constexpr (OP == MADI64) asm volatile("v_mad_i64_i32 %0, vcc, %1, %2, %0" : "+v"(q[i]) : "v"(x), "v"(y) : "vcc");
+        if constexpr (OP == BITOP3) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x6c" : "+v"(r[i]) : "v"(x), "v"(y));
+        if constexpr (OP == CND64) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(r[i]) : "v"(x), "s"(mask));
+        if constexpr (OP == MULI24) asm volatile("v_mul_i32_i24 %0, %0, %1" : "+v"(r[i]) : "v"(x));
       }
     }
   }
@@ -122,5 +129,6 @@ int main() {
   run<ALIGNBIT>(ncu, dout, ghz); run<ADD3>(ncu, dout, ghz); run<LSHLADD64>(ncu, dout, ghz);
   run<FMA32>(ncu, dout, ghz); run<BFI>(ncu, dout, ghz);
   run<XOR>(ncu, dout, ghz); run<CNDMASK>(ncu, dout, ghz); run<ADDCO3>(ncu, dout, ghz); run<MADMIX>(ncu, dout, ghz); run<LSHR>(ncu, dout, ghz);
+  run<ASHR64>(ncu, dout, ghz); run<MADI64>(ncu, dout, ghz); run<BITOP3>(ncu, dout, ghz); run<CND64>(ncu, dout, ghz); run<MULI24>(ncu, dout, ghz);
   return 0;
 }
