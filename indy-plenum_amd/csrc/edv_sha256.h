@@ -81,8 +81,22 @@ EDV_HD void sha256_msg(uint32_t out[8], const uint8_t* m, uint64_t mlen) {
   uint32_t W[16];
 #pragma unroll 1
   for (uint64_t b = 0; b < nb; b++) {
+    if (64 * b + 64 <= mlen) {
+      // whole block inside the message (every block but the last one or two):
+      // plain funnel-shifted loads, none of the clamp/pad selects, which lower
+      // to v_cndmask_b32 with a VCC mask (~23 cycles each on gfx950)
+      const uintptr_t a = reinterpret_cast<uintptr_t>(m + 64 * b);
+      const uint32_t sh = uint32_t(a & 3);
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(a - sh);
+      uint32_t d[17];
 #pragma unroll
-    for (int t = 0; t < 16; t++) W[t] = msg_word32(m, mlen, 64 * b + 4 * t);
+      for (int t = 0; t < 17; t++) d[t] = p[t];
+#pragma unroll
+      for (int t = 0; t < 16; t++) W[t] = bswap32(uint32_t(((uint64_t(d[t + 1]) << 32) | d[t]) >> (8 * sh)));
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; t++) W[t] = msg_word32(m, mlen, 64 * b + 4 * t);
+    }
     if (b == nb - 1) {
       W[14] = uint32_t(mlen >> 29);
       W[15] = uint32_t(mlen << 3);
