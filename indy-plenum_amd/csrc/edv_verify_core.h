@@ -44,6 +44,21 @@ EDV_HD uint64_t msg_word(const uint8_t* m, uint64_t mlen, uint64_t q) {
   return be64_from_le_words(uint32_t(v), uint32_t(v >> 32));
 }
 
+// N big-endian SHA words of message bytes [q, q + 8N) that lie wholly inside the
+// message: funnel-shifted aligned loads, none of msg_word's clamp/pad selects.
+template <int N>
+EDV_HD void msg_words_full(uint64_t* W, const uint8_t* m, uint64_t q) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(m + q);
+  const uint32_t sh = uint32_t(a & 3);
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(a - sh);
+  uint32_t d[2 * N + 1];
+#pragma unroll
+  for (int t = 0; t < 2 * N + 1; t++) d[t] = p[t];
+#pragma unroll
+  for (int t = 0; t < N; t++)
+    W[t] = be64_from_le_words(alignbyte(d[2 * t + 1], d[2 * t], sh), alignbyte(d[2 * t + 2], d[2 * t + 1], sh));
+}
+
 // SHA-512(P || M) for a 32- or 64-byte prefix P given as little-endian words,
 // -> 16 little-endian words of the 64-byte digest.
 template <int PB>
@@ -57,15 +72,23 @@ EDV_HD void sha512_pm(uint32_t out[16], const uint32_t* P, const uint8_t* m, uin
   uint64_t W[16];
 #pragma unroll
   for (int t = 0; t < PW; t++) W[t] = be64_from_le_words(P[2 * t], P[2 * t + 1]);
+  if (mlen >= uint64_t(128 - PB)) {
+    msg_words_full<16 - PW>(W + PW, m, 0);
+  } else {
 #pragma unroll
-  for (int t = PW; t < 16; t++) W[t] = msg_word(m, mlen, uint64_t(8 * (t - PW)));
+    for (int t = PW; t < 16; t++) W[t] = msg_word(m, mlen, uint64_t(8 * (t - PW)));
+  }
   if (nb == 1) { W[14] = total >> 61; W[15] = total << 3; }
   sha512_compress(H, W);
 #pragma unroll 1
   for (uint64_t b = 1; b < nb; b++) {
     const uint64_t q0 = 128 * b - PB;
+    if (q0 + 128 <= mlen) {
+      msg_words_full<16>(W, m, q0);
+    } else {
 #pragma unroll
-    for (int t = 0; t < 16; t++) W[t] = msg_word(m, mlen, q0 + 8 * t);
+      for (int t = 0; t < 16; t++) W[t] = msg_word(m, mlen, q0 + 8 * t);
+    }
     if (b == nb - 1) { W[14] = total >> 61; W[15] = total << 3; }
     sha512_compress(H, W);
   }
