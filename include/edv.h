@@ -41,14 +41,21 @@ extern "C" {
 
 /*
  * Verify n detached signatures held in HOST memory; synchronous.
+ * Each device's shard is walked in sub-batches over four streams: H2D copies of
+ * one overlap the kernels of the others.  Inputs in pinned memory (e.g. from
+ * edv_host_alloc) are copied to the device directly; pageable inputs are first
+ * staged through the library's pinned buffers by a parallel memcpy
+ * (EDV_COPY_THREADS threads, default 8).
  *   sigs     n x 64 bytes (R || S), contiguous
  *   pks      n x 32 bytes (A), contiguous
  *   msgs     concatenated messages; message i = msgs[msg_off[i] .. msg_off[i+1])
  *   msg_off  n + 1 non-decreasing byte offsets
  *   accept   out: n bytes, 1 = accept, 0 = reject
- *   device_mask  bit d selects HIP device d; 0 = all visible devices.  The batch is
- *            split by request index into contiguous shards, one per device (no
- *            inter-device traffic; each shard's accept bytes land in its slice).
+ *   device_mask  bit d selects device d; 0 = all visible devices.  The batch is
+ *            split by request index into contiguous shards, one per device and
+ *            one host thread each (edv_shard_split: equal counts, or equal
+ *            estimated cost when SHA-512 block counts differ); no inter-device
+ *            traffic; each shard's accept bytes land in its slice.
  * Replaces: a loop of nacl_wrappers.Verifier.verify (nacl_wrappers.py:232-242).
  */
 int edv_verify_batch(const uint8_t *sigs, const uint8_t *pks, const uint8_t *msgs, const uint64_t *msg_off,
@@ -59,12 +66,26 @@ int edv_verify_batch(const uint8_t *sigs, const uint8_t *pks, const uint8_t *msg
  * asynchronous on `stream` (a hipStream_t, NULL = the library's own stream of
  * that device, which is then synchronised before returning).  Offsets are
  * absolute into d_msgs minus msg_base (so a shard may pass the global offset
- * array slice unchanged).  d_msgs must be readable 16 bytes past the last
- * message byte.
+ * array slice unchanged).
+ * Alignment (EDV_E_ARG otherwise): d_sigs and d_pks 16-byte aligned (read as
+ * 16-byte vectors), d_msg_off 8-byte aligned.  d_msgs may have any alignment:
+ * message bytes are read as aligned 32-bit words, so the kernels touch up to
+ * 3 bytes before a message start (never across a page) and up to 16 bytes past
+ * the last message byte, which must be readable.
+ * Launches on different streams never share the library's per-device scratch
+ * concurrently: each one is ordered after the previous user of the scratch.
  */
 int edv_verify_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
                          const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept,
                          int device, void *stream);
+
+/* Per-call SHA-512 length-bucket hint for the device paths (overrides the
+ * device mode of edv_set_length_buckets for this call only). */
+#define EDV_FLAG_UNIFORM_LENGTH 1u /* every message has the same SHA-512 block count: no buckets */
+#define EDV_FLAG_BUCKETS 2u        /* always bucket by block count */
+int edv_verify_batch_dev_flags(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
+                               const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept,
+                               int device, void *stream, uint32_t flags);
 
 /*
  * Batch SHA-256: out[32 i .. 32 i + 32) = SHA-256 of message i
@@ -94,7 +115,7 @@ int edv_sha256_batch_dev(const uint8_t *d_msgs, const uint64_t *d_msg_off, uint6
  */
 int edv_verify_batch_dev_pipelined(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
                                    const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept,
-                                   int device);
+                                   int device, uint32_t flags);
 /* Wait until every pipelined batch submitted on `device` has its verdicts. */
 int edv_pipeline_sync(int device);
 
@@ -146,8 +167,24 @@ int edv_sign_batch_dev(const uint8_t *d_seeds, const uint8_t *d_msgs, const uint
 int edv_stream(int device, void **out);
 int edv_sync(int device);
 
-/* Number of visible gfx950 devices (0 if none). */
+/* Number of visible gfx950 devices (0 if none).  EDV_VIRTUAL_DEVICES=k (a
+ * testing knob) presents k logical devices mapped round-robin onto the physical
+ * ones, each with its own context, so the multi-device path runs on one GPU. */
 int edv_device_count(void);
+
+/*
+ * The shard split edv_verify_batch uses (host only, no GPU needed): bounds[0..g]
+ * with shard k = requests [bounds[k], bounds[k+1]).  Equal request counts
+ * (n*k/g) when every message has the same SHA-512 block count; otherwise equal
+ * estimated cost, sum over the shard of (40 + SHA-512 blocks of R||A||M), where
+ * 40 blocks is the fixed per-verify work of SURVEY.md section 8d's W(m).
+ */
+int edv_shard_split(const uint64_t *msg_off, uint64_t n, uint32_t g, uint64_t *bounds);
+
+/* Pinned (page-locked, portable) host memory: inputs packed here are copied to
+ * the device by DMA without the staging memcpy. */
+int edv_host_alloc(uint64_t bytes, void **out);
+int edv_host_free(void *p);
 
 /* Device memory helpers so a host without PyTorch can stage inputs. */
 int edv_dev_alloc(int device, uint64_t bytes, void **out);

@@ -289,8 +289,24 @@ class CoreAuthMixin:
         other request goes through the Python plan, which raises exactly what
         the reference raises."""
         n = len(reqs)
+        whole = self._native_batch(reqs, verifier)
+        if whole is not None:
+            # one native call did host prep + the GPU verify for the common path
+            out, slow, rejected = whole
+            for k in rejected:
+                out[k] = InsufficientCorrectSignatures(0, 1)
+            if slow:
+                sub = [reqs[k] for k in slow]
+                for k, r in zip(slow, self._batch_planned(sub, [None] * len(sub), verifier)):
+                    out[k] = r
+            return out
+        return self._batch_planned(reqs, self._native_prep(reqs, verifier), verifier)
+
+    def _batch_planned(self, reqs, fast, verifier):
+        """authenticate_batch over per-request native prep results (`fast`,
+        None entries take the Python plan): one open_batch call, then replay."""
+        n = len(reqs)
         out = [None] * n
-        fast = self._native_prep(reqs, verifier)
         if fast is None:
             fast = [None] * n
         # fast requests: jobs 0..F-1, result [idr] or InsufficientCorrectSignatures(0, 1)
@@ -318,18 +334,32 @@ class CoreAuthMixin:
                 out[k] = ex
         return out
 
-    def _native_prep(self, reqs, verifier):
-        """_edvhost.prep_core_batch when this authenticator and verifier are the
-        stock ones (an override of any step it restates keeps the Python path)."""
+    def _stock(self, verifier):
+        """True when this authenticator and verifier are the stock ones (an
+        override of any step the native code restates keeps the Python path)."""
         cls = type(self)
-        if (_edvhost is None or verifier is not DidVerifier or not isinstance(getattr(self, "clients", None), dict)
-                or cls._prepare is not CoreAuthMixin._prepare
-                or cls.serializeForSig is not CoreAuthMixin.serializeForSig
-                or cls._plan_multi is not NaclAuthNr._plan_multi
-                or cls.getVerkey is not SimpleAuthNr.getVerkey
-                or base58._native is None):
+        return not (_edvhost is None or verifier is not DidVerifier
+                    or not isinstance(getattr(self, "clients", None), dict)
+                    or cls._prepare is not CoreAuthMixin._prepare
+                    or cls.serializeForSig is not CoreAuthMixin.serializeForSig
+                    or cls._plan_multi is not NaclAuthNr._plan_multi
+                    or cls.getVerkey is not SimpleAuthNr.getVerkey
+                    or base58._native is None)
+
+    def _native_prep(self, reqs, verifier):
+        """_edvhost.prep_core_batch for the stock authenticator, else None."""
+        if not self._stock(verifier):
             return None
         return _edvhost.prep_core_batch(reqs, self.clients, self.excluded_from_signing)
+
+    def _native_batch(self, reqs, verifier):
+        """_edvhost.auth_core_batch (host prep on PREP_THREADS threads + one
+        edv_verify_batch call, GIL released) -> (out, slow, rejected), for the
+        stock authenticator and the stock verify entry point, else None."""
+        if not self._stock(verifier) or not edv.native_batch_enabled():
+            return None
+        return _edvhost.auth_core_batch(reqs, self.clients, self.excluded_from_signing, edv.verify_address(),
+                                        edv.BATCH_DEVICE_MASK, edv.PREP_THREADS)
 
     # requests are only read, never mutated, by the stock batch path above
     def batch_reads_only(self):

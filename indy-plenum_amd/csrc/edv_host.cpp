@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -411,7 +412,291 @@ PyObject* py_prep_core_batch(PyObject*, PyObject* args) {
   return out;
 }
 
+// --------------------------------------------- whole-batch CoreAuthNr (f-1)
+// auth_core_batch(reqs, clients, excluded, verify_addr, device_mask, threads)
+//   -> (out, slow, rejected)
+// The single-signature fast path of prep_core_batch, done for a whole batch in
+// one call with the GPU verify inside it:
+//   phase A (GIL held)  type checks, in-memory verkey lookup (SimpleAuthNr.getVerkey,
+//                       client_authn.py:148-160), SigningSerializer bytes
+//                       (client_authn.py:248-252) appended to the message arena;
+//   phase B (no GIL)    base58 of signatures, identifiers and verkeys
+//                       (client_authn.py:94, verifier.py:26-52) on `threads`
+//                       threads, packed straight into the arena;
+//   phase C (no GIL)    one call of the C-ABI verifier at verify_addr
+//                       (edv_verify_batch, include/edv.h);
+//   phase D (GIL held)  out[k] = [identifier] for an accepted request.
+// slow: request indices outside the fast path (out[k] stays None; the caller's
+// Python plan handles them, with every exception the reference raises);
+// rejected: fast-path requests whose signature did not verify (the caller sets
+// InsufficientCorrectSignatures(0, 1), the replay result of a failed single
+// signature, client_authn.py:110-112).
+typedef int (*verify_fn_t)(const uint8_t*, const uint8_t*, const uint8_t*, const uint64_t*, uint64_t, uint8_t*,
+                           uint32_t);
+typedef int (*host_alloc_t)(uint64_t, void**);
+typedef int (*host_free_t)(void*);
+host_alloc_t g_alloc = nullptr;
+host_free_t g_free = nullptr;
+
+// A reusable arena for one batch (page-locked through the library's
+// edv_host_alloc when set_host_allocator was called, so the verifier DMAs it
+// without a staging copy).  Only touched with the GIL held or by the call that
+// owns it.
+struct Arena {
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  bool pinned = false;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap) return true;
+    release();
+    bytes += bytes / 4 + 4096;
+    void* q = nullptr;
+    if (g_alloc && g_alloc(uint64_t(bytes), &q) == 0 && q) {
+      pinned = true;
+    } else {
+      q = malloc(bytes);
+      pinned = false;
+      if (!q) return false;
+    }
+    p = static_cast<uint8_t*>(q);
+    cap = bytes;
+    return true;
+  }
+  void release() {
+    if (p) {
+      if (pinned && g_free) g_free(p);
+      else if (!pinned) free(p);
+    }
+    p = nullptr;
+    cap = 0;
+  }
+};
+std::vector<Arena*> g_arenas;  // free list (GIL held)
+
+Arena* take_arena() {
+  if (g_arenas.empty()) return new Arena();
+  Arena* a = g_arenas.back();
+  g_arenas.pop_back();
+  return a;
+}
+
+PyObject* py_set_host_allocator(PyObject*, PyObject* args) {
+  unsigned long long a, f;
+  if (!PyArg_ParseTuple(args, "KK", &a, &f)) return nullptr;
+  for (Arena* x : g_arenas) { x->release(); delete x; }
+  g_arenas.clear();
+  g_alloc = reinterpret_cast<host_alloc_t>(uintptr_t(a));
+  g_free = reinterpret_cast<host_free_t>(uintptr_t(f));
+  Py_RETURN_NONE;
+}
+
+struct FastItem {
+  Py_ssize_t k;
+  PyObject *idr, *sig_o, *vk_o;  // referenced while the GIL is released (the decode reads their text)
+  const uint8_t *sig, *idr_p, *vk_p;
+  size_t sig_n, idr_n, vk_n;
+  int vk_kind;  // 0 cryptonym (no verkey), 1 '~' abbreviated, 2 full verkey
+};
+
+inline bool ascii_str(PyObject* o, const uint8_t** p, size_t* n) {
+  if (!PyUnicode_CheckExact(o) || PyUnicode_READY(o) < 0 || !PyUnicode_IS_ASCII(o)) return false;
+  *p = reinterpret_cast<const uint8_t*>(PyUnicode_DATA(o));
+  *n = size_t(PyUnicode_GET_LENGTH(o));
+  return true;
+}
+
+// phase A for one request: false = not the fast path (nothing appended)
+int collect_one(PyObject* req, PyObject* clients, PyObject* excluded, Py_ssize_t k, std::string& msgs,
+                FastItem* it) {
+  if (!PyDict_CheckExact(req)) return 0;
+  PyObject* idr = PyDict_GetItemString(req, "identifier");
+  PyObject* sig = PyDict_GetItemString(req, "signature");
+  if (!idr || !sig) return 0;
+  it->k = k;
+  it->idr = idr;
+  if (!ascii_str(sig, &it->sig, &it->sig_n) || !ascii_str(idr, &it->idr_p, &it->idr_n) || it->sig_n == 0 ||
+      it->idr_n == 0)
+    return 0;
+  PyObject* nym = PyDict_GetItemWithError(clients, idr);
+  if (!nym) return PyErr_Occurred() ? -1 : 0;
+  if (!PyDict_CheckExact(nym) || PyDict_GET_SIZE(nym) == 0) return 0;
+  PyObject* verkey = PyDict_GetItemString(nym, "verkey");
+  if (!verkey || !ascii_str(verkey, &it->vk_p, &it->vk_n)) return 0;
+  it->sig_o = sig;
+  it->vk_o = verkey;
+  if (it->vk_n == 0) {
+    it->vk_kind = 0;
+  } else if (it->vk_p[0] == '~') {
+    it->vk_kind = 1;
+    it->vk_p++;
+    it->vk_n--;
+  } else {
+    it->vk_kind = 2;
+  }
+  const size_t mark = msgs.size();
+  const int r = ser(req, 0, excluded, msgs);
+  if (r != 1) {
+    msgs.resize(mark);
+    return r;
+  }
+  return 1;
+}
+
+// phase B for one item: signature -> sig64, key -> pk32; false = not the fast path
+bool decode_one(const FastItem& it, uint8_t* sig64, uint8_t* pk32) {
+  std::string s, a, b;
+  if (!b58_decode(it.sig, it.sig_n, true, &s) || s.size() != 64) return false;
+  memcpy(sig64, s.data(), 64);
+  if (it.vk_kind == 2) {
+    if (!b58_decode(it.vk_p, it.vk_n, true, &a) || a.size() != 32) return false;
+    memcpy(pk32, a.data(), 32);
+    return true;
+  }
+  if (!b58_decode(it.idr_p, it.idr_n, true, &a)) return false;
+  if (it.vk_kind == 0) {
+    if (a.size() != 32) return false;  // cryptonym: the identifier is the key
+    memcpy(pk32, a.data(), 32);
+    return true;
+  }
+  if (!b58_decode(it.vk_p, it.vk_n, true, &b) || a.size() + b.size() != 32) return false;
+  memcpy(pk32, a.data(), a.size());
+  memcpy(pk32 + a.size(), b.data(), b.size());
+  return true;
+}
+
+PyObject* py_auth_core_batch(PyObject*, PyObject* args) {
+  PyObject *reqs, *clients, *excluded;
+  unsigned long long vaddr;
+  unsigned int mask;
+  int threads;
+  if (!PyArg_ParseTuple(args, "OO!OKIi", &reqs, &PyDict_Type, &clients, &excluded, &vaddr, &mask, &threads))
+    return nullptr;
+  const verify_fn_t verify = reinterpret_cast<verify_fn_t>(uintptr_t(vaddr));
+  PyObject* seq = PySequence_Fast(reqs, "auth_core_batch needs a sequence of requests");
+  if (!seq) return nullptr;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  PyObject *out = nullptr, *slow = nullptr, *rejected = nullptr, *res = nullptr;
+  std::vector<FastItem> items;
+  items.reserve(size_t(n));
+  std::string msgs;
+  std::vector<uint64_t> moff(1, 0);
+  std::vector<Py_ssize_t> slow_idx;
+  // phase A
+  for (Py_ssize_t k = 0; k < n; k++) {
+    FastItem it;
+    const int r = collect_one(PySequence_Fast_GET_ITEM(seq, k), clients, excluded, k, msgs, &it);
+    if (r < 0) { Py_DECREF(seq); return nullptr; }
+    if (r == 0) { slow_idx.push_back(k); continue; }
+    Py_INCREF(it.idr);
+    Py_INCREF(it.sig_o);
+    Py_INCREF(it.vk_o);
+    items.push_back(it);
+    moff.push_back(uint64_t(msgs.size()));
+  }
+  struct Hold {  // drop the item references on every return path (GIL held)
+    std::vector<FastItem>& v;
+    ~Hold() {
+      for (FastItem& it : v) { Py_DECREF(it.idr); Py_DECREF(it.sig_o); Py_DECREF(it.vk_o); }
+    }
+  } hold{items};
+  const size_t nf = items.size();
+  std::vector<uint8_t> good(nf, 1);
+  Arena* ar = take_arena();
+  // arena layout: sigs 64 nf | pks 32 nf | off 8 (nf + 1) | msgs (+64 slack) | accept nf
+  const size_t o_pk = 64 * nf, o_off = o_pk + 32 * nf, o_msg = o_off + 8 * (nf + 1),
+               o_acc = o_msg + ((msgs.size() + 64 + 63) / 64) * 64;
+  int rc = 0;
+  if (nf && !ar->ensure(o_acc + nf)) {
+    g_arenas.push_back(ar);
+    Py_DECREF(seq);
+    return PyErr_NoMemory();
+  }
+  if (nf) {
+    uint8_t* base = ar->p;
+    Py_BEGIN_ALLOW_THREADS
+    // phase B: decode on T threads; the message bytes and offsets are copied beside
+    const int T = nf < 2048 ? 1 : std::max(1, std::min(threads, 32));
+    auto part = [&](int t) {
+      const size_t lo = nf * size_t(t) / size_t(T), hi = nf * size_t(t + 1) / size_t(T);
+      for (size_t i = lo; i < hi; i++)
+        if (!decode_one(items[i], base + 64 * i, base + o_pk + 32 * i)) {
+          good[i] = 0;
+          memset(base + 64 * i, 0, 64);  // verified for nothing; the verdict is ignored
+          memset(base + o_pk + 32 * i, 0, 32);
+        }
+      const size_t mlo = msgs.size() * size_t(t) / size_t(T), mhi = msgs.size() * size_t(t + 1) / size_t(T);
+      memcpy(base + o_msg + mlo, msgs.data() + mlo, mhi - mlo);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; t++) th.emplace_back(part, t);
+    part(0);
+    for (auto& x : th) x.join();
+    memcpy(base + o_off, moff.data(), 8 * (nf + 1));
+    memset(base + o_msg + msgs.size(), 0, 64);
+    // phase C: one device call
+    rc = verify(base, base + o_pk, base + o_msg, reinterpret_cast<const uint64_t*>(base + o_off), uint64_t(nf),
+                base + o_acc, mask);
+    Py_END_ALLOW_THREADS
+  }
+  if (rc != 0) {
+    g_arenas.push_back(ar);
+    Py_DECREF(seq);
+    PyErr_Format(PyExc_RuntimeError, "edv_verify_batch failed (%d)", rc);
+    return nullptr;
+  }
+  // phase D
+  out = PyList_New(n);
+  slow = PyList_New(0);
+  rejected = PyList_New(0);
+  if (!out || !slow || !rejected) goto fail;
+  for (Py_ssize_t k = 0; k < n; k++) {
+    Py_INCREF(Py_None);
+    PyList_SET_ITEM(out, k, Py_None);
+  }
+  for (Py_ssize_t k : slow_idx) {
+    PyObject* v = PyLong_FromSsize_t(k);
+    if (!v || PyList_Append(slow, v) < 0) { Py_XDECREF(v); goto fail; }
+    Py_DECREF(v);
+  }
+  for (size_t i = 0; i < nf; i++) {
+    const FastItem& it = items[i];
+    if (!good[i]) {
+      PyObject* v = PyLong_FromSsize_t(it.k);
+      if (!v || PyList_Append(slow, v) < 0) { Py_XDECREF(v); goto fail; }
+      Py_DECREF(v);
+    } else if (ar->p[o_acc + i]) {
+      PyObject* l = PyList_New(1);
+      if (!l) goto fail;
+      Py_INCREF(it.idr);
+      PyList_SET_ITEM(l, 0, it.idr);
+      PyObject* old = PyList_GET_ITEM(out, it.k);
+      PyList_SET_ITEM(out, it.k, l);
+      Py_DECREF(old);
+    } else {
+      PyObject* v = PyLong_FromSsize_t(it.k);
+      if (!v || PyList_Append(rejected, v) < 0) { Py_XDECREF(v); goto fail; }
+      Py_DECREF(v);
+    }
+  }
+  if (PyList_Sort(slow) < 0) goto fail;
+  res = Py_BuildValue("(NNN)", out, slow, rejected);
+  g_arenas.push_back(ar);
+  Py_DECREF(seq);
+  return res;
+fail:
+  Py_XDECREF(out);
+  Py_XDECREF(slow);
+  Py_XDECREF(rejected);
+  g_arenas.push_back(ar);
+  Py_DECREF(seq);
+  return nullptr;
+}
+
 PyMethodDef kMethods[] = {
+    {"auth_core_batch", py_auth_core_batch, METH_VARARGS,
+     "whole-batch CoreAuthNr fast path with the GPU verify inside: (out, slow, rejected)"},
+    {"set_host_allocator", py_set_host_allocator, METH_VARARGS,
+     "page-locked arena allocator (edv_host_alloc, edv_host_free addresses)"},
     {"prep_core_batch", py_prep_core_batch, METH_VARARGS, "CoreAuthNr single-signature fast path (None = Python)"},
     {"b58decode", py_b58decode, METH_O, "base58 1.0.0 b58decode fast path (NotImplemented = use Python)"},
     {"b58encode", py_b58encode, METH_O, "base58 1.0.0 b58encode fast path (NotImplemented = use Python)"},

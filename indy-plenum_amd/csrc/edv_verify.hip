@@ -107,10 +107,16 @@ struct GlobalBTab {
     const int4* p = reinterpret_cast<const int4*>(w + j * kBStride);
     int32_t t[32];
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
+    for (int i = 0; i < 7; i++) {
       const int4 v = p[i];
       t[4 * i] = v.x; t[4 * i + 1] = v.y; t[4 * i + 2] = v.z; t[4 * i + 3] = v.w;
     }
+    // words 28, 29 only: loading the two pad words as well let the register
+    // allocator reuse their VGPRs as temporaries, which forced a vmcnt wait
+    // on the whole entry before the window's doublings (the opaque offset
+    // keeps LLVM from widening this 8-byte load back to 16 bytes)
+    const int2 v = *reinterpret_cast<const int2*>(w + j * kBStride + opaque_i32(28));
+    t[28] = v.x; t[29] = v.y;
     return precomp_from_words(t);
   }
 };
@@ -160,6 +166,16 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   for (int k = 0; k < 8; k++) {
     hd[k] = a.st.dig[uint64_t(k) * a.st.cap + j];
     sd[k] = a.st.dig[uint64_t(8 + k) * a.st.cap + j];
+  }
+  // Settle the digit loads here, once: the digit registers are shifted inside
+  // the window loop, and the waitcnt pass, merging the loop's back edge with
+  // loads still pending from the preheader, otherwise inserts vmcnt waits at
+  // the loop head and right after the B-table loads (so every fourth window
+  // stalled on its table reads; 9.5 % of wave cycles in SQ_WAIT_ANY).
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    hd[k] = uint32_t(opaque_i32(int32_t(hd[k])));
+    sd[k] = uint32_t(opaque_i32(int32_t(sd[k])));
   }
   const GlobalATab at{a.st.atab + j * kAWords};
   const GlobalBTab bt{a.btab};
@@ -295,6 +311,19 @@ int set_err(int code, const char* what, hipError_t e = hipSuccess) {
     if (e_ != hipSuccess) return set_err(EDV_E_HIP, what, e_); \
   } while (0)
 
+// HIP events of a measurement helper, destroyed on every return path
+struct Events {
+  hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+  int n = 0;
+  int create(int k) {
+    for (n = 0; n < k; n++) HIPOK(hipEventCreate(&e[n]), "event");
+    return 0;
+  }
+  ~Events() {
+    for (int i = 0; i < n; i++) (void)hipEventDestroy(e[i]);
+  }
+};
+
 struct DevBuf {
   void* p = nullptr;
   uint64_t cap = 0;
@@ -308,13 +337,38 @@ struct DevBuf {
   }
 };
 
+// Pinned (page-locked, portable) host memory: staging of pageable inputs
+struct PinnedBuf {
+  void* p = nullptr;
+  uint64_t cap = 0;
+  int ensure(uint64_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) (void)hipHostFree(p);
+    p = nullptr; cap = 0;
+    bytes = bytes + bytes / 4 + 4096;  // headroom: message bytes vary from call to call
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) {
+      p = nullptr;
+      return set_err(EDV_E_OOM, "hipHostMalloc");
+    }
+    cap = bytes;
+    return 0;
+  }
+};
+
+// Host path: a shard is walked in sub-batches, round-robin over kQ streams,
+// so the H2D copy of one sub-batch overlaps the kernels of the others and
+// several sub-batches share the chip at once (a 64k batch split 4 ways still
+// fills every SIMD).  Sub-batch stream q uses scratch slots [q*P, (q+1)*P) of
+// the chunk state.
+constexpr int kQ = 4;
+
 // One set of per-chunk state buffers (ChunkState storage + bucket permutation).
 struct ChunkBufs {
   DevBuf atab, dig, alive;  // ChunkState storage for `chunk` signatures (~400 MB at 2^18)
-  DevBuf perm, bucket_ctr;  // length-bucket permutation of a chunk; histogram + cursors
+  DevBuf perm, bucket_ctr;  // length-bucket permutation of a chunk; histogram + cursors (one set per stream)
   int ensure(uint64_t chunk) {
     if (atab.ensure(chunk * kAWords * 4) || dig.ensure(chunk * 16 * 4) || alive.ensure(chunk) ||
-        perm.ensure(chunk * 4) || bucket_ctr.ensure(2 * kBuckets * 4))
+        perm.ensure(chunk * 4) || bucket_ctr.ensure(uint64_t(kQ) * 2 * kBuckets * 4))
       return EDV_E_OOM;
     return 0;
   }
@@ -323,14 +377,25 @@ struct ChunkBufs {
 struct DevCtx {
   std::mutex mu;
   bool ready = false;
-  int dev = -1;
-  hipStream_t stream = nullptr;
+  int dev = -1;                    // logical device (edv_* device index)
+  int phys = -1;                   // HIP device it runs on
+  hipStream_t stream = nullptr;    // the library stream (edv_stream)
   int32_t* btab = nullptr;
+  bool btab_built = false;
   int32_t* comb = nullptr;         // signer comb table, built on first edv_sign_* call
   uint64_t chunk = kChunkDefault;  // EDV_CHUNK overrides (tests exercise chunk seams)
   int length_buckets = 2;          // 0 never, 1 always, 2 auto (edv_set_length_buckets)
-  ChunkBufs st;                    // state of the ordinary (one stream) path
+  ChunkBufs st;                    // scratch of the ordinary paths
+  // st_done: recorded after the last kernel that used `st`, on whatever stream
+  // that was; every later user waits for it first, so launches on different
+  // caller streams never share the scratch concurrently.
+  hipEvent_t st_done = nullptr;
+  // host path (edv_verify_batch)
+  hipStream_t hs[kQ] = {};
+  hipEvent_t hs_staged[kQ] = {};   // pinned slot q may be refilled once its H2D copies are done
+  hipEvent_t hs_end[kQ] = {};
   DevBuf sigs, pks, msgs, off, acc;
+  PinnedBuf stage[kQ], acc_host;
   // Pipelined submission (edv_verify_batch_dev_pipelined): two state sets, a
   // prep stream and a main stream, so the prep kernel of batch k+1 runs on the
   // SIMDs beside the main kernel of batch k.  prep_done[b] orders main after its
@@ -347,33 +412,57 @@ std::mutex g_mu;
 std::vector<DevCtx*> g_ctx;
 int g_ndev = -1;
 
+// Logical devices.  Normally one per visible HIP device.  EDV_VIRTUAL_DEVICES=k
+// (testing knob) presents k logical devices mapped round-robin onto the
+// physical ones, each with its own context, streams and buffers, so the
+// multi-device host path (one thread per device, shard split, error
+// propagation) runs on a one-GPU box exactly as it does on eight GPUs.
 int device_count_locked() {
   if (g_ndev >= 0) return g_ndev;
   int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
-  g_ndev = n;
-  g_ctx.resize(n, nullptr);
-  for (int i = 0; i < n; i++) g_ctx[i] = new DevCtx();
-  return n;
+  if (hipGetDeviceCount(&n) != hipSuccess) { (void)hipGetLastError(); n = 0; }
+  int logical = n;
+  if (const char* e = getenv("EDV_VIRTUAL_DEVICES")) {
+    const long v = strtol(e, nullptr, 10);
+    if (n > 0 && v > 0 && v <= 32) logical = int(v);
+  }
+  g_ndev = logical;
+  g_ctx.resize(logical, nullptr);
+  for (int i = 0; i < logical; i++) {
+    g_ctx[i] = new DevCtx();
+    g_ctx[i]->dev = i;
+    g_ctx[i]->phys = n > 0 ? i % n : 0;
+  }
+  return logical;
 }
 
-int ctx_init(DevCtx& c, int dev) {
+// Idempotent: a failure part-way leaves what was created in place and the next
+// call resumes from there (no second stream or table per retry).
+int ctx_init(DevCtx& c) {
   if (c.ready) return 0;
-  c.dev = dev;
-  HIPOK(hipSetDevice(dev), "hipSetDevice");
+  HIPOK(hipSetDevice(c.phys), "hipSetDevice");
   hipDeviceProp_t prop;
-  HIPOK(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties");
+  HIPOK(hipGetDeviceProperties(&prop, c.phys), "hipGetDeviceProperties");
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return set_err(EDV_E_NODEV, "device is not gfx950");
-  HIPOK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking), "hipStreamCreate");
+  if (!c.stream) HIPOK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking), "hipStreamCreate");
+  for (int q = 0; q < kQ; q++) {
+    if (!c.hs[q]) HIPOK(hipStreamCreateWithFlags(&c.hs[q], hipStreamNonBlocking), "hipStreamCreate");
+    if (!c.hs_staged[q]) HIPOK(hipEventCreateWithFlags(&c.hs_staged[q], hipEventDisableTiming), "event");
+    if (!c.hs_end[q]) HIPOK(hipEventCreateWithFlags(&c.hs_end[q], hipEventDisableTiming), "event");
+  }
+  if (!c.st_done) HIPOK(hipEventCreateWithFlags(&c.st_done, hipEventDisableTiming), "event");
   if (const char* e = getenv("EDV_CHUNK")) {
     const uint64_t v = strtoull(e, nullptr, 10);
     if (v >= kBlock && v <= (uint64_t(1) << 24)) c.chunk = (v / kBlock) * kBlock;
   }
   if (c.st.ensure(c.chunk)) return EDV_E_OOM;
-  HIPOK(hipMalloc(&c.btab, kBEntries * kBStride * 4), "hipMalloc btab");
-  edv_btab_kernel<<<(kBEntries + 63) / 64, 64, 0, c.stream>>>(c.btab);
-  HIPOK(hipGetLastError(), "btab launch");
-  HIPOK(hipStreamSynchronize(c.stream), "btab sync");
+  if (!c.btab) HIPOK(hipMalloc(&c.btab, kBEntries * kBStride * 4), "hipMalloc btab");
+  if (!c.btab_built) {
+    edv_btab_kernel<<<(kBEntries + 63) / 64, 64, 0, c.stream>>>(c.btab);
+    HIPOK(hipGetLastError(), "btab launch");
+    HIPOK(hipStreamSynchronize(c.stream), "btab sync");
+    c.btab_built = true;
+  }
   c.ready = true;
   return 0;
 }
@@ -386,8 +475,31 @@ DevCtx* get_ctx(int dev, int* err) {
   return g_ctx[dev];
 }
 
+// Lock a device's context, initialise it and make its HIP device current.
+struct CtxLock {
+  DevCtx* c = nullptr;
+  std::unique_lock<std::mutex> lk;
+  int err = 0;
+  explicit CtxLock(int device) {
+    c = get_ctx(device, &err);
+    if (!c) return;
+    lk = std::unique_lock<std::mutex>(c->mu);
+    if ((err = ctx_init(*c))) return;
+    if (hipSetDevice(c->phys) != hipSuccess) err = set_err(EDV_E_HIP, "hipSetDevice");
+  }
+};
+
+int phys_of(int device, int* phys) {
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  *phys = c->phys;
+  return 0;
+}
+
 VerifyArgs make_args(const DevCtx& c, ChunkBufs& b, const uint8_t* d_sigs, const uint8_t* d_pks,
-                     const uint8_t* d_msgs, const uint64_t* d_off, uint64_t msg_base, uint8_t* d_accept, bool bucket) {
+                     const uint8_t* d_msgs, const uint64_t* d_off, uint64_t msg_base, uint8_t* d_accept, bool bucket,
+                     uint64_t slot0 = 0) {
   VerifyArgs va;
   va.sigs = reinterpret_cast<const uint32_t*>(d_sigs);
   va.pks = reinterpret_cast<const uint32_t*>(d_pks);
@@ -395,23 +507,24 @@ VerifyArgs make_args(const DevCtx& c, ChunkBufs& b, const uint8_t* d_sigs, const
   va.off = d_off;
   va.msg_base = msg_base;
   va.accept = d_accept;
-  va.st = ChunkState{static_cast<int32_t*>(b.atab.p), static_cast<uint32_t*>(b.dig.p), static_cast<uint8_t*>(b.alive.p),
-                     c.chunk, bucket ? static_cast<uint32_t*>(b.perm.p) : nullptr};
+  // slots [slot0, slot0 + n) of the chunk scratch (dig stays indexed w * cap + slot)
+  va.st = ChunkState{static_cast<int32_t*>(b.atab.p) + slot0 * kAWords, static_cast<uint32_t*>(b.dig.p) + slot0,
+                     static_cast<uint8_t*>(b.alive.p) + slot0, c.chunk,
+                     bucket ? static_cast<uint32_t*>(b.perm.p) + slot0 : nullptr};
   va.btab = c.btab;
   va.base = 0;
   va.n = 0;
   return va;
 }
 
-// [length buckets,] prep kernel of one chunk on stream s
-int launch_prep(ChunkBufs& b, const VerifyArgs& va, const uint64_t* d_off, bool bucket, hipStream_t s) {
+// [length buckets,] prep kernel of one chunk on stream s (ctr: this stream's histogram + cursors)
+int launch_prep(uint32_t* ctr, const VerifyArgs& va, const uint64_t* d_off, bool bucket, hipStream_t s) {
   const unsigned blocks = unsigned((va.n + kBlock - 1) / kBlock);
   if (bucket) {
-    uint32_t* hist = static_cast<uint32_t*>(b.bucket_ctr.p);
-    HIPOK(hipMemsetAsync(hist, 0, 2 * kBuckets * 4, s), "memset buckets");
-    edv_bucket_hist_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, va.base, va.n, hist);
-    edv_bucket_scatter_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, va.base, va.n, hist, hist + kBuckets,
-                                                                     static_cast<uint32_t*>(b.perm.p));
+    HIPOK(hipMemsetAsync(ctr, 0, 2 * kBuckets * 4, s), "memset buckets");
+    edv_bucket_hist_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, va.base, va.n, ctr);
+    edv_bucket_scatter_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, va.base, va.n, ctr, ctr + kBuckets,
+                                                                     const_cast<uint32_t*>(va.st.perm));
     HIPOK(hipGetLastError(), "bucket launch");
   }
   edv_prep_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
@@ -424,48 +537,48 @@ int launch_main(const VerifyArgs& va, hipStream_t s) {
   HIPOK(hipGetLastError(), "main launch");
   return 0;
 }
+uint32_t* bucket_ctr(ChunkBufs& b, int q) { return static_cast<uint32_t*>(b.bucket_ctr.p) + q * 2 * kBuckets; }
 
 // Length buckets cost three small launches per chunk (memset, histogram,
-// scatter); a caller that knows its messages share one SHA-512 block count
-// turns them off with edv_set_length_buckets(device, 0).  Verdicts never depend on it.
-static bool bucketing_enabled(const DevCtx& c, bool want, bool host_path = false) {
+// scatter).  Per call: EDV_FLAG_UNIFORM_LENGTH turns them off,
+// EDV_FLAG_BUCKETS forces them; otherwise the device mode decides
+// (edv_set_length_buckets).  Verdicts never depend on it.
+bool bucketing_enabled(const DevCtx& c, uint32_t flags) {
   static const bool no_bucket = getenv("EDV_NO_BUCKET") != nullptr;  // A/B measurement knob
-  if (no_bucket) return false;
-  if (host_path || c.length_buckets == 2) return want;  // the host path knows the lengths
-  return c.length_buckets == 1;
+  if (no_bucket || (flags & EDV_FLAG_UNIFORM_LENGTH)) return false;
+  if (flags & EDV_FLAG_BUCKETS) return true;
+  return c.length_buckets != 0;
 }
 
-// Ordinary path: launch on ctx stream or the given stream; caller holds c.mu.
-// The batch is walked in chunks of c.chunk signatures: [length buckets,] prep
-// kernel, main kernel, all in stream order.
+// Ordinary device path: launch on stream s; caller holds c.mu.  The batch is
+// walked in chunks of c.chunk signatures: [length buckets,] prep kernel, main
+// kernel, all in stream order, after every earlier user of the scratch.
 int launch(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_off,
-           uint64_t msg_base, uint64_t n, uint8_t* d_accept, hipStream_t s, bool bucket = true,
-           bool host_path = false) {
-  bucket = bucketing_enabled(c, bucket, host_path);
-  if (c.pipe_ready) {  // state set 0 of the pipeline is separate, but drain it so results stay ordered
-    HIPOK(hipStreamSynchronize(c.sp), "pipeline sync");
-    HIPOK(hipStreamSynchronize(c.sm), "pipeline sync");
-  }
+           uint64_t msg_base, uint64_t n, uint8_t* d_accept, hipStream_t s, uint32_t flags) {
+  if (n == 0) return 0;
+  const bool bucket = bucketing_enabled(c, flags);
+  HIPOK(hipStreamWaitEvent(s, c.st_done, 0), "wait scratch");
   VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, msg_base, d_accept, bucket);
   int err;
   for (uint64_t base = 0; base < n; base += c.chunk) {
     va.base = base;
     va.n = (n - base) < c.chunk ? (n - base) : c.chunk;
-    if ((err = launch_prep(c.st, va, d_off, bucket, s)) || (err = launch_main(va, s))) return err;
+    if ((err = launch_prep(bucket_ctr(c.st, 0), va, d_off, bucket, s)) || (err = launch_main(va, s))) return err;
   }
+  HIPOK(hipEventRecord(c.st_done, s), "record scratch");
   return 0;
 }
 
 int pipe_init(DevCtx& c) {
   if (c.pipe_ready) return 0;
   if (c.pst[0].ensure(c.chunk) || c.pst[1].ensure(c.chunk)) return EDV_E_OOM;
-  HIPOK(hipStreamCreateWithFlags(&c.sp, hipStreamNonBlocking), "hipStreamCreate");
-  HIPOK(hipStreamCreateWithFlags(&c.sm, hipStreamNonBlocking), "hipStreamCreate");
+  if (!c.sp) HIPOK(hipStreamCreateWithFlags(&c.sp, hipStreamNonBlocking), "hipStreamCreate");
+  if (!c.sm) HIPOK(hipStreamCreateWithFlags(&c.sm, hipStreamNonBlocking), "hipStreamCreate");
   for (int b = 0; b < 2; b++) {
-    HIPOK(hipEventCreateWithFlags(&c.prep_done[b], hipEventDisableTiming), "event");
-    HIPOK(hipEventCreateWithFlags(&c.main_done[b], hipEventDisableTiming), "event");
+    if (!c.prep_done[b]) HIPOK(hipEventCreateWithFlags(&c.prep_done[b], hipEventDisableTiming), "event");
+    if (!c.main_done[b]) HIPOK(hipEventCreateWithFlags(&c.main_done[b], hipEventDisableTiming), "event");
   }
-  HIPOK(hipEventCreateWithFlags(&c.inputs_ready, hipEventDisableTiming), "event");
+  if (!c.inputs_ready) HIPOK(hipEventCreateWithFlags(&c.inputs_ready, hipEventDisableTiming), "event");
   c.pipe_ready = true;
   return 0;
 }
@@ -475,10 +588,10 @@ int pipe_init(DevCtx& c) {
 // prep.  Work already queued on the library stream (e.g. the batch signer)
 // is ordered before the first prep.  Caller holds c.mu.
 int launch_pipelined(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
-                     const uint64_t* d_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept) {
+                     const uint64_t* d_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, uint32_t flags) {
   int err;
   if ((err = pipe_init(c))) return err;
-  const bool bucket = bucketing_enabled(c, true);
+  const bool bucket = bucketing_enabled(c, flags);
   HIPOK(hipEventRecord(c.inputs_ready, c.stream), "record");
   HIPOK(hipStreamWaitEvent(c.sp, c.inputs_ready, 0), "wait");
   for (uint64_t base = 0; base < n; base += c.chunk) {
@@ -489,7 +602,7 @@ int launch_pipelined(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, con
     va.base = base;
     va.n = (n - base) < c.chunk ? (n - base) : c.chunk;
     if (c.pending[b]) HIPOK(hipStreamWaitEvent(c.sp, c.main_done[b], 0), "wait");
-    if ((err = launch_prep(cb, va, d_off, bucket, c.sp))) return err;
+    if ((err = launch_prep(bucket_ctr(cb, 0), va, d_off, bucket, c.sp))) return err;
     HIPOK(hipEventRecord(c.prep_done[b], c.sp), "record");
     HIPOK(hipStreamWaitEvent(c.sm, c.prep_done[b], 0), "wait");
     if ((err = launch_main(va, c.sm))) return err;
@@ -499,37 +612,155 @@ int launch_pipelined(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, con
   return 0;
 }
 
-// one shard on one device, host buffers
-int run_shard(int dev, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off, uint64_t lo,
+// Drain every stream of the context (before scratch is reallocated).
+int drain(DevCtx& c) {
+  HIPOK(hipStreamSynchronize(c.stream), "stream sync");
+  HIPOK(hipEventSynchronize(c.st_done), "scratch sync");
+  for (int q = 0; q < kQ; q++) HIPOK(hipStreamSynchronize(c.hs[q]), "stream sync");
+  if (c.pipe_ready) {
+    HIPOK(hipStreamSynchronize(c.sp), "pipeline sync");
+    HIPOK(hipStreamSynchronize(c.sm), "pipeline sync");
+    c.pending[0] = c.pending[1] = false;
+  }
+  return 0;
+}
+
+// ---- host memory: pinned detection and a parallel staging copy
+bool is_pinned(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: not an error for us
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost;
+}
+
+struct Seg {
+  uint8_t* dst;
+  const uint8_t* src;
+  uint64_t n;
+};
+int copy_threads() {
+  static const int t = [] {
+    if (const char* e = getenv("EDV_COPY_THREADS")) {
+      const long v = strtol(e, nullptr, 10);
+      if (v >= 1 && v <= 64) return int(v);
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    return int(hw >= 16 ? 8 : (hw >= 2 ? hw / 2 : 1));
+  }();
+  return t;
+}
+// memcpy of several segments, split evenly by bytes over up to copy_threads()
+// threads (a single thread below 4 MiB)
+void par_copy(const std::vector<Seg>& segs) {
+  uint64_t total = 0;
+  for (const Seg& s : segs) total += s.n;
+  const int T = total < (uint64_t(4) << 20) ? 1 : copy_threads();
+  auto part = [&](int t) {
+    const uint64_t lo = total * t / T, hi = total * (t + 1) / T;
+    uint64_t pos = 0;
+    for (const Seg& s : segs) {
+      const uint64_t a = lo > pos ? lo - pos : 0, b = hi - pos < s.n ? hi - pos : s.n;
+      if (hi > pos && a < b && a < s.n) memcpy(s.dst + a, s.src + a, b - a);
+      pos += s.n;
+      if (pos >= hi) break;
+    }
+  };
+  if (T == 1) { part(0); return; }
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back(part, t);
+  part(0);
+  for (auto& x : th) x.join();
+}
+
+uint64_t sha512_blocks(const uint64_t* off, uint64_t i) { return (64 + (off[i + 1] - off[i]) + 17 + 127) / 128; }
+
+// One shard on one device, host buffers: sub-batches of P requests go round
+// robin over the kQ host-path streams; per sub-batch: H2D copies (straight
+// from the caller's memory when it is pinned, else through this stream's
+// pinned slot, filled by a parallel memcpy while earlier sub-batches run),
+// [length buckets,] prep, main, D2H of its accept bytes.  Caller holds c.mu.
+int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off, uint64_t lo,
               uint64_t hi, uint8_t* accept) {
-  int err = 0;
-  DevCtx* c = get_ctx(dev, &err);
-  if (!c) return err;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((err = ctx_init(*c, dev))) return err;
-  HIPOK(hipSetDevice(dev), "hipSetDevice");
   const uint64_t n = hi - lo;
   if (n == 0) return 0;
+  int Q = c.chunk >= uint64_t(kQ) * kBlock ? kQ : 1;
+  if (const char* e = getenv("EDV_HOST_STREAMS")) {  // A/B measurement knob (1..4)
+    const int v = atoi(e);
+    if (v >= 1 && v <= Q) Q = v;
+  }
+  const uint64_t pmax = c.chunk / Q;
+  uint64_t P = (n + Q - 1) / Q;
+  P = ((P + 63) / 64) * 64;
+  if (P > pmax) P = pmax;
+  const uint64_t nsub = (n + P - 1) / P;
   const uint64_t mbase = off[lo], mbytes = off[hi] - off[lo];
-  if (c->sigs.ensure(n * 64) || c->pks.ensure(n * 32) || c->msgs.ensure(mbytes + 64) ||
-      c->off.ensure((n + 1) * 8) || c->acc.ensure(n))
+  if (c.sigs.ensure(n * 64) || c.pks.ensure(n * 32) || c.msgs.ensure(mbytes + 64) ||
+      c.off.ensure((n + nsub) * 8) || c.acc.ensure(n))
     return EDV_E_OOM;
-  HIPOK(hipMemcpyAsync(c->sigs.p, sigs + 64 * lo, n * 64, hipMemcpyHostToDevice, c->stream), "h2d sigs");
-  HIPOK(hipMemcpyAsync(c->pks.p, pks + 32 * lo, n * 32, hipMemcpyHostToDevice, c->stream), "h2d pks");
-  if (mbytes) HIPOK(hipMemcpyAsync(c->msgs.p, msgs + mbase, mbytes, hipMemcpyHostToDevice, c->stream), "h2d msgs");
-  HIPOK(hipMemcpyAsync(c->off.p, off + lo, (n + 1) * 8, hipMemcpyHostToDevice, c->stream), "h2d off");
+  const bool pinned = is_pinned(sigs + 64 * lo) && is_pinned(pks + 32 * lo) && is_pinned(off + lo) &&
+                      (mbytes == 0 || is_pinned(msgs + mbase));
+  const bool acc_pinned = is_pinned(accept + lo);
+  if (!acc_pinned && c.acc_host.ensure(n)) return EDV_E_OOM;
   // bucket by SHA block count only when the shard's messages differ in block count
   bool varied = false;
   {
-    const uint64_t nb0 = (64 + off[lo + 1] - off[lo] + 17 + 127) / 128;
-    for (uint64_t i = lo + 1; i < hi && !varied; i++) varied = (64 + off[i + 1] - off[i] + 17 + 127) / 128 != nb0;
+    const uint64_t nb0 = sha512_blocks(off, lo);
+    for (uint64_t i = lo + 1; i < hi && !varied; i++) varied = sha512_blocks(off, i) != nb0;
   }
-  if ((err = launch(*c, static_cast<uint8_t*>(c->sigs.p), static_cast<uint8_t*>(c->pks.p),
-                    static_cast<uint8_t*>(c->msgs.p), static_cast<uint64_t*>(c->off.p), mbase, n,
-                    static_cast<uint8_t*>(c->acc.p), c->stream, varied, true)))
-    return err;
-  HIPOK(hipMemcpyAsync(accept + lo, c->acc.p, n, hipMemcpyDeviceToHost, c->stream), "d2h accept");
-  HIPOK(hipStreamSynchronize(c->stream), "stream sync");
+  const uint32_t flags = varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH;
+  uint8_t* d_sigs = static_cast<uint8_t*>(c.sigs.p);
+  uint8_t* d_pks = static_cast<uint8_t*>(c.pks.p);
+  uint8_t* d_msgs = static_cast<uint8_t*>(c.msgs.p);
+  uint64_t* d_off = static_cast<uint64_t*>(c.off.p);
+  uint8_t* d_acc = static_cast<uint8_t*>(c.acc.p);
+  uint8_t* h_acc = acc_pinned ? accept + lo : static_cast<uint8_t*>(c.acc_host.p);
+  for (int q = 0; q < Q; q++) HIPOK(hipStreamWaitEvent(c.hs[q], c.st_done, 0), "wait scratch");
+  int err;
+  for (uint64_t k = 0; k < nsub; k++) {
+    const int q = int(k % Q);
+    hipStream_t s = c.hs[q];
+    const uint64_t a = lo + k * P, b = (a + P) < hi ? (a + P) : hi, cnt = b - a;
+    const uint64_t mA = off[a], mB = off[b];
+    // sub-batch k's offsets live at d_off + (a - lo) + k: one private n+1 window each
+    uint64_t* d_o = d_off + (a - lo) + k;
+    const uint8_t *src_s = sigs + 64 * a, *src_p = pks + 32 * a, *src_m = msgs + mA;
+    const uint64_t* src_o = off + a;
+    if (!pinned) {
+      PinnedBuf& sl = c.stage[q];
+      HIPOK(hipEventSynchronize(c.hs_staged[q]), "stage wait");  // the slot's previous H2D is done
+      if (sl.ensure(cnt * 96 + (cnt + 1) * 8 + (mB - mA))) return EDV_E_OOM;
+      uint8_t* p = static_cast<uint8_t*>(sl.p);
+      par_copy({{p, src_s, cnt * 64}, {p + cnt * 64, src_p, cnt * 32},
+                {p + cnt * 96, reinterpret_cast<const uint8_t*>(src_o), (cnt + 1) * 8},
+                {p + cnt * 96 + (cnt + 1) * 8, src_m, mB - mA}});
+      src_s = p;
+      src_p = p + cnt * 64;
+      src_o = reinterpret_cast<const uint64_t*>(p + cnt * 96);
+      src_m = p + cnt * 96 + (cnt + 1) * 8;
+    }
+    HIPOK(hipMemcpyAsync(d_sigs + 64 * (a - lo), src_s, cnt * 64, hipMemcpyHostToDevice, s), "h2d sigs");
+    HIPOK(hipMemcpyAsync(d_pks + 32 * (a - lo), src_p, cnt * 32, hipMemcpyHostToDevice, s), "h2d pks");
+    HIPOK(hipMemcpyAsync(d_o, src_o, (cnt + 1) * 8, hipMemcpyHostToDevice, s), "h2d off");
+    if (mB > mA) HIPOK(hipMemcpyAsync(d_msgs + (mA - mbase), src_m, mB - mA, hipMemcpyHostToDevice, s), "h2d msgs");
+    if (!pinned) HIPOK(hipEventRecord(c.hs_staged[q], s), "record");
+    const bool bucket = bucketing_enabled(c, flags);
+    VerifyArgs va = make_args(c, c.st, d_sigs + 64 * (a - lo), d_pks + 32 * (a - lo), d_msgs, d_o, mbase,
+                              d_acc + (a - lo), bucket, uint64_t(q) * pmax);
+    va.n = cnt;
+    if ((err = launch_prep(bucket_ctr(c.st, q), va, d_o, bucket, s)) || (err = launch_main(va, s))) return err;
+    HIPOK(hipMemcpyAsync(h_acc + (a - lo), d_acc + (a - lo), cnt, hipMemcpyDeviceToHost, s), "d2h accept");
+  }
+  // join the sub-batch streams into the library stream: the scratch's next user waits for all of them
+  for (int q = 0; q < Q; q++) {
+    HIPOK(hipEventRecord(c.hs_end[q], c.hs[q]), "record");
+    HIPOK(hipStreamWaitEvent(c.stream, c.hs_end[q], 0), "wait");
+  }
+  HIPOK(hipEventRecord(c.st_done, c.stream), "record scratch");
+  HIPOK(hipStreamSynchronize(c.stream), "stream sync");
+  if (!acc_pinned) memcpy(accept + lo, h_acc, n);
   return 0;
 }
 
@@ -542,32 +773,61 @@ int launch_sha256(const uint8_t* d_msgs, const uint64_t* d_off, uint64_t msg_bas
   return 0;
 }
 
-// SHA-256 digests of messages [lo, hi) on one device, host buffers
-int run_digest_shard(int dev, const uint8_t* msgs, const uint64_t* off, uint64_t lo, uint64_t hi, uint8_t* out) {
-  int err = 0;
-  DevCtx* c = get_ctx(dev, &err);
-  if (!c) return err;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((err = ctx_init(*c, dev))) return err;
-  HIPOK(hipSetDevice(dev), "hipSetDevice");
+// SHA-256 digests of messages [lo, hi) on one device, host buffers; caller holds c.mu
+int run_digest_shard(DevCtx& c, const uint8_t* msgs, const uint64_t* off, uint64_t lo, uint64_t hi, uint8_t* out) {
   const uint64_t n = hi - lo;
   if (n == 0) return 0;
   const uint64_t mbase = off[lo], mbytes = off[hi] - off[lo];
-  if (c->msgs.ensure(mbytes + 64) || c->off.ensure((n + 1) * 8) || c->sigs.ensure(n * 32)) return EDV_E_OOM;
-  if (mbytes) HIPOK(hipMemcpyAsync(c->msgs.p, msgs + mbase, mbytes, hipMemcpyHostToDevice, c->stream), "h2d msgs");
-  HIPOK(hipMemcpyAsync(c->off.p, off + lo, (n + 1) * 8, hipMemcpyHostToDevice, c->stream), "h2d off");
-  if ((err = launch_sha256(static_cast<uint8_t*>(c->msgs.p), static_cast<uint64_t*>(c->off.p), mbase, n,
-                           static_cast<uint8_t*>(c->sigs.p), c->stream)))
+  if (c.msgs.ensure(mbytes + 64) || c.off.ensure((n + 1) * 8) || c.sigs.ensure(n * 32)) return EDV_E_OOM;
+  // the host verify path shares these buffers; it finishes (synchronously) under the same lock
+  if (mbytes) HIPOK(hipMemcpyAsync(c.msgs.p, msgs + mbase, mbytes, hipMemcpyHostToDevice, c.stream), "h2d msgs");
+  HIPOK(hipMemcpyAsync(c.off.p, off + lo, (n + 1) * 8, hipMemcpyHostToDevice, c.stream), "h2d off");
+  int err;
+  if ((err = launch_sha256(static_cast<uint8_t*>(c.msgs.p), static_cast<uint64_t*>(c.off.p), mbase, n,
+                           static_cast<uint8_t*>(c.sigs.p), c.stream)))
     return err;
-  HIPOK(hipMemcpyAsync(out + 32 * lo, c->sigs.p, n * 32, hipMemcpyDeviceToHost, c->stream), "d2h digests");
-  HIPOK(hipStreamSynchronize(c->stream), "stream sync");
+  HIPOK(hipMemcpyAsync(out + 32 * lo, c.sigs.p, n * 32, hipMemcpyDeviceToHost, c.stream), "d2h digests");
+  HIPOK(hipStreamSynchronize(c.stream), "stream sync");
   return 0;
 }
 
+// Per-verify cost in SHA-512-block units for the shard split: W(m) of SURVEY.md
+// section 8d is 217,600 + 5,500 * blocks INT32 ops, i.e. ~40 blocks' worth of
+// fixed work (decompress, scalar multiplication, encode) per signature.
+constexpr uint64_t kVerifyBlocks = 40;
+
+// Split [0, n) into g contiguous shards by request index: equal counts when
+// every message has the same SHA-512 block count (C2/C3), else equal estimated
+// cost, sum over the shard of (kVerifyBlocks + blocks_i) (C4).
+void shard_bounds(const uint64_t* off, uint64_t n, uint32_t g, uint64_t* b) {
+  b[0] = 0;
+  b[g] = n;
+  bool uniform = true;
+  if (n > 0) {
+    const uint64_t nb0 = sha512_blocks(off, 0);
+    for (uint64_t i = 1; i < n && uniform; i++) uniform = sha512_blocks(off, i) == nb0;
+  }
+  if (uniform) {
+    for (uint32_t k = 1; k < g; k++) b[k] = uint64_t((unsigned __int128)n * k / g);
+    return;
+  }
+  // total cost = kVerifyBlocks * n + sum of blocks; shard k starts at the first
+  // request whose prefix cost reaches total * k / g
+  unsigned __int128 total = 0;
+  for (uint64_t i = 0; i < n; i++) total += kVerifyBlocks + sha512_blocks(off, i);
+  unsigned __int128 pre = 0;
+  uint32_t k = 1;
+  for (uint64_t i = 0; i < n && k < g; i++) {
+    while (k < g && pre * g >= total * k) b[k++] = i;
+    pre += kVerifyBlocks + sha512_blocks(off, i);
+  }
+  while (k < g) b[k++] = n;
+}
+
 // Validate a host batch and split [0, n) over the devices of device_mask, one
-// host thread per device; shard(dev, lo, hi) does the work.
+// host thread per device; shard(ctx, lo, hi) does the work under the context lock.
 template <class Shard>
-int for_each_shard(uint64_t n, uint32_t device_mask, Shard shard) {
+int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard shard) {
   int ndev;
   {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -577,20 +837,41 @@ int for_each_shard(uint64_t n, uint32_t device_mask, Shard shard) {
   for (int d = 0; d < ndev && d < 32; d++)
     if (device_mask == 0 || (device_mask >> d) & 1u) devs.push_back(d);
   if (devs.empty()) return set_err(EDV_E_NODEV, "no device selected / visible");
-  const uint64_t g = devs.size();
-  if (g == 1) return shard(devs[0], uint64_t(0), n);
+  const uint32_t g = uint32_t(devs.size());
+  std::vector<uint64_t> bounds(g + 1);
+  shard_bounds(off, n, g, bounds.data());
+  auto one = [&](int dev, uint64_t lo, uint64_t hi) {
+    CtxLock cl(dev);
+    if (cl.err) return cl.err;
+    return shard(*cl.c, lo, hi);
+  };
+  if (g == 1) return one(devs[0], 0, n);
   std::vector<int> rc(g, 0);
   std::vector<std::string> errs(g);
   std::vector<std::thread> th;
-  for (uint64_t k = 0; k < g; k++) {
+  for (uint32_t k = 0; k < g; k++) {
     th.emplace_back([&, k]() {
-      rc[k] = shard(devs[k], n * k / g, n * (k + 1) / g);
+      rc[k] = one(devs[k], bounds[k], bounds[k + 1]);
       errs[k] = g_err;
     });
   }
   for (auto& t : th) t.join();
-  for (uint64_t k = 0; k < g; k++)
+  for (uint32_t k = 0; k < g; k++)
     if (rc[k]) { g_err = errs[k]; return rc[k]; }
+  return 0;
+}
+
+int check_offsets(const uint64_t* msg_off, uint64_t n) {
+  for (uint64_t i = 0; i < n; i++)
+    if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_E_ARG, "msg_off not non-decreasing");
+  return 0;
+}
+
+// device pointers the kernels read as 16-byte vectors must be 16-byte aligned
+int check_dev_align(const void* d_sigs, const void* d_pks, const void* d_off) {
+  if ((reinterpret_cast<uintptr_t>(d_sigs) & 15) || (reinterpret_cast<uintptr_t>(d_pks) & 15) ||
+      (reinterpret_cast<uintptr_t>(d_off) & 7))
+    return set_err(EDV_E_ARG, "d_sigs / d_pks must be 16-byte and d_msg_off 8-byte aligned");
   return 0;
 }
 
@@ -599,12 +880,21 @@ int for_each_shard(uint64_t n, uint32_t device_mask, Shard shard) {
 // ------------------------------------------------------------------ C-ABI
 extern "C" {
 
-const char* edv_version(void) { return "edv 0.1.0 gfx950"; }
+const char* edv_version(void) { return "edv 0.2.0 gfx950"; }
 const char* edv_last_error(void) { return g_err.c_str(); }
 
 int edv_device_count(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   return device_count_locked();
+}
+
+int edv_shard_split(const uint64_t* msg_off, uint64_t n, uint32_t g, uint64_t* bounds) {
+  g_err.clear();
+  if (!bounds || g == 0 || (n > 0 && !msg_off)) return set_err(EDV_E_ARG, "null pointer / zero shards");
+  int err;
+  if (n > 0 && (err = check_offsets(msg_off, n))) return err;
+  shard_bounds(msg_off, n, g, bounds);
+  return 0;
 }
 
 int edv_verify_batch(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* msg_off,
@@ -613,10 +903,10 @@ int edv_verify_batch(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msg
   if (n == 0) return 0;
   if (!sigs || !pks || !msg_off || !accept) return set_err(EDV_E_ARG, "null pointer");
   if (!msgs && msg_off[n] != msg_off[0]) return set_err(EDV_E_ARG, "null msgs");
-  for (uint64_t i = 0; i < n; i++)
-    if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_E_ARG, "msg_off not non-decreasing");
-  return for_each_shard(n, device_mask, [&](int dev, uint64_t lo, uint64_t hi) {
-    return run_shard(dev, sigs, pks, msgs, msg_off, lo, hi, accept);
+  int err;
+  if ((err = check_offsets(msg_off, n))) return err;
+  return for_each_shard(msg_off, n, device_mask, [&](DevCtx& c, uint64_t lo, uint64_t hi) {
+    return run_shard(c, sigs, pks, msgs, msg_off, lo, hi, accept);
   });
 }
 
@@ -625,24 +915,35 @@ int edv_sha256_batch(const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, u
   if (n == 0) return 0;
   if (!msg_off || !out) return set_err(EDV_E_ARG, "null pointer");
   if (!msgs && msg_off[n] != msg_off[0]) return set_err(EDV_E_ARG, "null msgs");
-  for (uint64_t i = 0; i < n; i++)
-    if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_E_ARG, "msg_off not non-decreasing");
-  return for_each_shard(n, device_mask, [&](int dev, uint64_t lo, uint64_t hi) {
-    return run_digest_shard(dev, msgs, msg_off, lo, hi, out);
+  int err;
+  if ((err = check_offsets(msg_off, n))) return err;
+  return for_each_shard(msg_off, n, device_mask, [&](DevCtx& c, uint64_t lo, uint64_t hi) {
+    return run_digest_shard(c, msgs, msg_off, lo, hi, out);
   });
 }
 
 int edv_sha256_batch_dev(const uint8_t* d_msgs, const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n,
                          uint8_t* d_out, int device, void* stream) {
   g_err.clear();
-  int err = 0;
-  DevCtx* c = get_ctx(device, &err);
-  if (!c) return err;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((err = ctx_init(*c, device))) return err;
-  HIPOK(hipSetDevice(device), "hipSetDevice");
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : cl.c->stream;
+  int err;
   if ((err = launch_sha256(d_msgs, d_msg_off, msg_base, n, d_out, s))) return err;
+  if (!stream) HIPOK(hipStreamSynchronize(s), "stream sync");
+  return 0;
+}
+
+int edv_verify_batch_dev_flags(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
+                               const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, int device,
+                               void* stream, uint32_t flags) {
+  g_err.clear();
+  int err;
+  if ((err = check_dev_align(d_sigs, d_pks, d_msg_off))) return err;
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : cl.c->stream;
+  if ((err = launch(*cl.c, d_sigs, d_pks, d_msgs, d_msg_off, msg_base, n, d_accept, s, flags))) return err;
   if (!stream) HIPOK(hipStreamSynchronize(s), "stream sync");
   return 0;
 }
@@ -650,41 +951,26 @@ int edv_sha256_batch_dev(const uint8_t* d_msgs, const uint64_t* d_msg_off, uint6
 int edv_verify_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
                          const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, int device,
                          void* stream) {
-  g_err.clear();
-  int err = 0;
-  DevCtx* c = get_ctx(device, &err);
-  if (!c) return err;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((err = ctx_init(*c, device))) return err;
-  HIPOK(hipSetDevice(device), "hipSetDevice");
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
-  if ((err = launch(*c, d_sigs, d_pks, d_msgs, d_msg_off, msg_base, n, d_accept, s))) return err;
-  if (!stream) HIPOK(hipStreamSynchronize(s), "stream sync");
-  return 0;
+  return edv_verify_batch_dev_flags(d_sigs, d_pks, d_msgs, d_msg_off, msg_base, n, d_accept, device, stream, 0);
 }
 
 int edv_verify_batch_dev_pipelined(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
                                    const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept,
-                                   int device) {
+                                   int device, uint32_t flags) {
   g_err.clear();
-  int err = 0;
-  DevCtx* c = get_ctx(device, &err);
-  if (!c) return err;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((err = ctx_init(*c, device))) return err;
-  HIPOK(hipSetDevice(device), "hipSetDevice");
+  int err;
+  if ((err = check_dev_align(d_sigs, d_pks, d_msg_off))) return err;
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
   if (n == 0) return 0;
-  return launch_pipelined(*c, d_sigs, d_pks, d_msgs, d_msg_off, msg_base, n, d_accept);
+  return launch_pipelined(*cl.c, d_sigs, d_pks, d_msgs, d_msg_off, msg_base, n, d_accept, flags);
 }
 
 int edv_pipeline_sync(int device) {
   g_err.clear();
-  int err = 0;
-  DevCtx* c = get_ctx(device, &err);
-  if (!c) return err;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((err = ctx_init(*c, device))) return err;
-  HIPOK(hipSetDevice(device), "hipSetDevice");
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  DevCtx* c = cl.c;
   if (!c->pipe_ready) return 0;
   HIPOK(hipStreamSynchronize(c->sp), "pipeline sync");
   HIPOK(hipStreamSynchronize(c->sm), "pipeline sync");
@@ -696,47 +982,50 @@ int edv_time_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_
                        const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, int device,
                        int iters, float* ms_out) {
   g_err.clear();
-  int err = 0;
-  DevCtx* c = get_ctx(device, &err);
-  if (!c) return err;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((err = ctx_init(*c, device))) return err;
-  HIPOK(hipSetDevice(device), "hipSetDevice");
-  hipEvent_t e0, e1;
-  HIPOK(hipEventCreate(&e0), "event");
-  HIPOK(hipEventCreate(&e1), "event");
-  HIPOK(hipEventRecord(e0, c->stream), "record");
+  int err;
+  if ((err = check_dev_align(d_sigs, d_pks, d_msg_off))) return err;
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  DevCtx* c = cl.c;
+  Events ev;
+  if ((err = ev.create(2))) return err;
+  HIPOK(hipEventRecord(ev.e[0], c->stream), "record");
   for (int it = 0; it < iters; it++)
-    if ((err = launch(*c, d_sigs, d_pks, d_msgs, d_msg_off, msg_base, n, d_accept, c->stream))) return err;
-  HIPOK(hipEventRecord(e1, c->stream), "record");
-  HIPOK(hipEventSynchronize(e1), "event sync");
+    if ((err = launch(*c, d_sigs, d_pks, d_msgs, d_msg_off, msg_base, n, d_accept, c->stream, 0))) return err;
+  HIPOK(hipEventRecord(ev.e[1], c->stream), "record");
+  HIPOK(hipEventSynchronize(ev.e[1]), "event sync");
   float ms = 0;
-  HIPOK(hipEventElapsedTime(&ms, e0, e1), "elapsed");
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  HIPOK(hipEventElapsedTime(&ms, ev.e[0], ev.e[1]), "elapsed");
   if (ms_out) *ms_out = ms;
   return 0;
 }
 
 static int ensure_comb(DevCtx& c) {
   if (c.comb) return 0;
-  HIPOK(hipMalloc(&c.comb, uint64_t(kCombRows) * kCombEntries * kBStride * 4), "hipMalloc comb");
+  int32_t* p = nullptr;
+  HIPOK(hipMalloc(&p, uint64_t(kCombRows) * kCombEntries * kBStride * 4), "hipMalloc comb");
   const int total = kCombRows * kCombEntries;
-  edv_comb_kernel<<<(total + 63) / 64, 64, 0, c.stream>>>(c.comb);
-  HIPOK(hipGetLastError(), "comb launch");
-  HIPOK(hipStreamSynchronize(c.stream), "comb sync");
+  edv_comb_kernel<<<(total + 63) / 64, 64, 0, c.stream>>>(p);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    return set_err(EDV_E_HIP, "comb table", e);
+  }
+  c.comb = p;
   return 0;
 }
 
 int edv_sign_batch_dev(const uint8_t* d_seeds, const uint8_t* d_msgs, const uint64_t* d_msg_off, uint64_t msg_base,
                        uint64_t n, uint8_t* d_pks, uint8_t* d_sigs, int device, void* stream) {
   g_err.clear();
-  int err = 0;
-  DevCtx* c = get_ctx(device, &err);
-  if (!c) return err;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((err = ctx_init(*c, device))) return err;
-  HIPOK(hipSetDevice(device), "hipSetDevice");
+  if ((reinterpret_cast<uintptr_t>(d_seeds) & 15) || (reinterpret_cast<uintptr_t>(d_pks) & 15) ||
+      (reinterpret_cast<uintptr_t>(d_sigs) & 15))
+    return set_err(EDV_E_ARG, "d_seeds / d_pks / d_sigs must be 16-byte aligned");
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  DevCtx* c = cl.c;
+  int err;
   if ((err = ensure_comb(*c))) return err;
   if (n == 0) return 0;
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
@@ -751,42 +1040,29 @@ int edv_sign_batch_dev(const uint8_t* d_seeds, const uint8_t* d_msgs, const uint
 
 int edv_stream(int device, void** out) {
   g_err.clear();
-  int err = 0;
-  DevCtx* c = get_ctx(device, &err);
-  if (!c) return err;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((err = ctx_init(*c, device))) return err;
-  *out = static_cast<void*>(c->stream);
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  *out = static_cast<void*>(cl.c->stream);
   return 0;
 }
 
 int edv_sync(int device) {
   g_err.clear();
-  int err = 0;
-  DevCtx* c = get_ctx(device, &err);
-  if (!c) return err;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((err = ctx_init(*c, device))) return err;
-  HIPOK(hipSetDevice(device), "hipSetDevice");
-  HIPOK(hipStreamSynchronize(c->stream), "stream sync");
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  HIPOK(hipStreamSynchronize(cl.c->stream), "stream sync");
   return 0;
 }
 
 int edv_set_chunk(int device, uint64_t chunk) {
   g_err.clear();
-  int err = 0;
-  DevCtx* c = get_ctx(device, &err);
-  if (!c) return err;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((err = ctx_init(*c, device))) return err;
-  HIPOK(hipSetDevice(device), "hipSetDevice");
-  HIPOK(hipStreamSynchronize(c->stream), "stream sync");
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  DevCtx* c = cl.c;
   if (chunk == 0) chunk = kChunkDefault;
   if (chunk < kBlock || chunk > (uint64_t(1) << 24)) return set_err(EDV_E_ARG, "chunk out of range");
-  if (c->pipe_ready) {
-    HIPOK(hipStreamSynchronize(c->sp), "pipeline sync");
-    HIPOK(hipStreamSynchronize(c->sm), "pipeline sync");
-  }
+  int err;
+  if ((err = drain(*c))) return err;  // nothing may still use the scratch being reallocated
   c->chunk = (chunk / kBlock) * kBlock;
   if (c->st.ensure(c->chunk)) return EDV_E_OOM;
   if (c->pipe_ready && (c->pst[0].ensure(c->chunk) || c->pst[1].ensure(c->chunk))) return EDV_E_OOM;
@@ -808,75 +1084,94 @@ int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uin
                           const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, int device,
                           int iters, float* ms_prep, float* ms_main) {
   g_err.clear();
-  int err = 0;
-  DevCtx* c = get_ctx(device, &err);
-  if (!c) return err;
-  std::lock_guard<std::mutex> lk(c->mu);
-  if ((err = ctx_init(*c, device))) return err;
-  HIPOK(hipSetDevice(device), "hipSetDevice");
-  if (n == 0 || n > c->chunk) return set_err(EDV_E_ARG, "profile needs 0 < n <= chunk");
-  VerifyArgs va;
-  va.sigs = reinterpret_cast<const uint32_t*>(d_sigs);
-  va.pks = reinterpret_cast<const uint32_t*>(d_pks);
-  va.msgs = d_msgs;
-  va.off = d_msg_off;
-  va.msg_base = msg_base;
-  va.accept = d_accept;
-  va.st = ChunkState{static_cast<int32_t*>(c->st.atab.p), static_cast<uint32_t*>(c->st.dig.p),
-                     static_cast<uint8_t*>(c->st.alive.p), c->chunk, static_cast<uint32_t*>(c->st.perm.p)};
-  va.btab = c->btab;
-  va.base = 0;
-  uint32_t* hist = static_cast<uint32_t*>(c->st.bucket_ctr.p);
-  const bool bucket = bucketing_enabled(*c, true);
-  if (!bucket) va.st.perm = nullptr;
+  int err;
+  if ((err = check_dev_align(d_sigs, d_pks, d_msg_off))) return err;
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  DevCtx* c = cl.c;
+  if (n == 0 || n > c->chunk || iters <= 0) return set_err(EDV_E_ARG, "profile needs 0 < n <= chunk, iters > 0");
+  const bool bucket = bucketing_enabled(*c, 0);
+  VerifyArgs va = make_args(*c, c->st, d_sigs, d_pks, d_msgs, d_msg_off, msg_base, d_accept, bucket);
   va.n = n;
+  uint32_t* hist = bucket_ctr(c->st, 0);
   const unsigned blocks = unsigned((n + kBlock - 1) / kBlock);
-  hipEvent_t ev[3];
-  for (auto& e : ev) HIPOK(hipEventCreate(&e), "event");
+  Events ev;
+  if ((err = ev.create(3))) return err;
+  HIPOK(hipStreamWaitEvent(c->stream, c->st_done, 0), "wait scratch");
   float tp = 0, tm = 0;
   for (int it = 0; it < iters; it++) {
     if (bucket) {
       HIPOK(hipMemsetAsync(hist, 0, 2 * kBuckets * 4, c->stream), "memset buckets");
       edv_bucket_hist_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(d_msg_off, 0, n, hist);
       edv_bucket_scatter_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(d_msg_off, 0, n, hist, hist + kBuckets,
-                                                                               static_cast<uint32_t*>(c->st.perm.p));
+                                                                               const_cast<uint32_t*>(va.st.perm));
     }
-    HIPOK(hipEventRecord(ev[0], c->stream), "record");
+    HIPOK(hipEventRecord(ev.e[0], c->stream), "record");
     edv_prep_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(va);
-    HIPOK(hipEventRecord(ev[1], c->stream), "record");
+    HIPOK(hipEventRecord(ev.e[1], c->stream), "record");
     edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(va);
-    HIPOK(hipEventRecord(ev[2], c->stream), "record");
-    HIPOK(hipEventSynchronize(ev[2]), "event sync");
+    HIPOK(hipEventRecord(ev.e[2], c->stream), "record");
+    HIPOK(hipEventSynchronize(ev.e[2]), "event sync");
     float a = 0, b = 0;
-    HIPOK(hipEventElapsedTime(&a, ev[0], ev[1]), "elapsed");
-    HIPOK(hipEventElapsedTime(&b, ev[1], ev[2]), "elapsed");
+    HIPOK(hipEventElapsedTime(&a, ev.e[0], ev.e[1]), "elapsed");
+    HIPOK(hipEventElapsedTime(&b, ev.e[1], ev.e[2]), "elapsed");
     tp += a;
     tm += b;
   }
-  for (auto& e : ev) (void)hipEventDestroy(e);
+  HIPOK(hipEventRecord(c->st_done, c->stream), "record scratch");
   if (ms_prep) *ms_prep = tp / iters;
   if (ms_main) *ms_main = tm / iters;
   return 0;
 }
 
 int edv_dev_alloc(int device, uint64_t bytes, void** out) {
-  HIPOK(hipSetDevice(device), "hipSetDevice");
+  int phys, err;
+  if ((err = phys_of(device, &phys))) return err;
+  HIPOK(hipSetDevice(phys), "hipSetDevice");
   HIPOK(hipMalloc(out, bytes ? bytes : 1), "hipMalloc");
   return 0;
 }
 int edv_dev_free(int device, void* p) {
-  HIPOK(hipSetDevice(device), "hipSetDevice");
+  int phys, err;
+  if ((err = phys_of(device, &phys))) return err;
+  HIPOK(hipSetDevice(phys), "hipSetDevice");
   HIPOK(hipFree(p), "hipFree");
   return 0;
 }
 int edv_h2d(int device, void* dst, const void* src, uint64_t bytes) {
-  HIPOK(hipSetDevice(device), "hipSetDevice");
+  int phys, err;
+  if ((err = phys_of(device, &phys))) return err;
+  HIPOK(hipSetDevice(phys), "hipSetDevice");
   HIPOK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), "hipMemcpy h2d");
   return 0;
 }
 int edv_d2h(int device, void* dst, const void* src, uint64_t bytes) {
-  HIPOK(hipSetDevice(device), "hipSetDevice");
+  int phys, err;
+  if ((err = phys_of(device, &phys))) return err;
+  HIPOK(hipSetDevice(phys), "hipSetDevice");
   HIPOK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), "hipMemcpy d2h");
+  return 0;
+}
+
+int edv_host_alloc(uint64_t bytes, void** out) {
+  g_err.clear();
+  if (!out) return set_err(EDV_E_ARG, "null pointer");
+  int n;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    n = device_count_locked();
+  }
+  if (n == 0) return set_err(EDV_E_NODEV, "no device visible");
+  HIPOK(hipSetDevice(g_ctx[0]->phys), "hipSetDevice");
+  if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) {
+    *out = nullptr;
+    return set_err(EDV_E_OOM, "hipHostMalloc");
+  }
+  return 0;
+}
+int edv_host_free(void* p) {
+  g_err.clear();
+  if (p) HIPOK(hipHostFree(p), "hipHostFree");
   return 0;
 }
 

@@ -247,6 +247,10 @@ EDV_HD bool main_one(const uint32_t R[8], uint32_t hd[8], uint32_t sd[8], const 
     if ((w & 3) == 0) {
       dB = int32_t(sd[7]) >> 16;
       shl256<16>(sd);
+      // shift before the loads are issued: scheduled after them, the shift's
+      // temporaries landed in the loads' destination VGPRs and forced a vmcnt
+      // wait right behind the loads
+      sched_fence();
       q = bt.entry(dB < 0 ? -dB : dB);
     }
     ge_p3 p3;

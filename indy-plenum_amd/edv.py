@@ -28,6 +28,8 @@ EDV_E_ARG = -1
 EDV_E_NODEV = -2
 EDV_E_HIP = -3
 EDV_E_OOM = -4
+FLAG_UNIFORM_LENGTH = 1  # every message has the same SHA-512 block count: no length buckets
+FLAG_BUCKETS = 2         # always bucket by SHA-512 block count
 
 
 class EdvUnavailable(RuntimeError):
@@ -66,7 +68,9 @@ def lib():
         h.edv_sha256_batch.restype = ctypes.c_int
         h.edv_sha256_batch_dev.argtypes = [vp, vp, u64, u64, vp, ctypes.c_int, vp]
         h.edv_sha256_batch_dev.restype = ctypes.c_int
-        h.edv_verify_batch_dev_pipelined.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int]
+        h.edv_verify_batch_dev_flags.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, vp, ctypes.c_uint32]
+        h.edv_verify_batch_dev_flags.restype = ctypes.c_int
+        h.edv_verify_batch_dev_pipelined.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_uint32]
         h.edv_verify_batch_dev_pipelined.restype = ctypes.c_int
         h.edv_pipeline_sync.argtypes = [ctypes.c_int]
         h.edv_pipeline_sync.restype = ctypes.c_int
@@ -86,6 +90,12 @@ def lib():
         h.edv_set_length_buckets.restype = ctypes.c_int
         h.edv_set_chunk.argtypes = [ctypes.c_int, u64]
         h.edv_set_chunk.restype = ctypes.c_int
+        h.edv_shard_split.argtypes = [vp, u64, ctypes.c_uint32, vp]
+        h.edv_shard_split.restype = ctypes.c_int
+        h.edv_host_alloc.argtypes = [u64, ctypes.POINTER(ctypes.c_void_p)]
+        h.edv_host_alloc.restype = ctypes.c_int
+        h.edv_host_free.argtypes = [vp]
+        h.edv_host_free.restype = ctypes.c_int
         h.edv_device_count.argtypes = []
         h.edv_device_count.restype = ctypes.c_int
         h.edv_dev_alloc.argtypes = [ctypes.c_int, u64, ctypes.POINTER(ctypes.c_void_p)]
@@ -232,6 +242,31 @@ def open_batch(items, device_mask: int = 0):
     return out
 
 
+_OPEN_BATCH = open_batch        # the genuine entry point (tests may monkeypatch open_batch)
+_verify_addr = None
+BATCH_DEVICE_MASK = 0          # devices used by the native whole-batch authenticator path
+PREP_THREADS = int(os.environ.get("EDV_PREP_THREADS", "0")) or max(1, min(8, (os.cpu_count() or 2) // 2))
+
+
+def verify_address() -> int:
+    """Address of edv_verify_batch (the native whole-batch authenticator calls it
+    with the GIL released); also hands edv_host_alloc/free to _edvhost so its
+    batch arenas are page-locked."""
+    global _verify_addr
+    if _verify_addr is None:
+        h = lib()
+        _edvhost.set_host_allocator(ctypes.cast(h.edv_host_alloc, ctypes.c_void_p).value,
+                                    ctypes.cast(h.edv_host_free, ctypes.c_void_p).value)
+        _verify_addr = ctypes.cast(h.edv_verify_batch, ctypes.c_void_p).value
+    return _verify_addr
+
+
+def native_batch_enabled() -> bool:
+    """The native whole-batch path calls edv_verify_batch itself, so it is used
+    only while open_batch is the genuine entry point."""
+    return open_batch is _OPEN_BATCH and os.environ.get("EDV_NATIVE_BATCH", "1") != "0"
+
+
 class DeviceBuffer:
     """A raw device allocation through the C-ABI (no PyTorch needed)."""
 
@@ -265,16 +300,56 @@ class DeviceBuffer:
             pass
 
 
-def verify_device(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, msg_base=0, stream=None):
-    """Device-resident verify (pointers are ints); async on `stream` if given."""
-    _check(lib().edv_verify_batch_dev(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, stream))
+def verify_device(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, msg_base=0, stream=None, flags=0):
+    """Device-resident verify (pointers are ints); async on `stream` if given.
+    flags: FLAG_UNIFORM_LENGTH / FLAG_BUCKETS (per-call length-bucket hint)."""
+    _check(lib().edv_verify_batch_dev_flags(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, stream,
+                                            flags))
 
 
-def verify_device_pipelined(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, msg_base=0):
+def verify_device_pipelined(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, msg_base=0, flags=0):
     """Enqueue a device-resident batch on the library's two-stream pipeline (the
     prep kernel of the next batch overlaps the main kernel of this one); the
     verdicts are in d_accept after pipeline_sync(device)."""
-    _check(lib().edv_verify_batch_dev_pipelined(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device))
+    _check(lib().edv_verify_batch_dev_pipelined(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device,
+                                                flags))
+
+
+def shard_split(offsets, g: int) -> np.ndarray:
+    """The C-ABI's shard split (edv_shard_split; host only, no GPU): g+1 bounds,
+    shard k = requests [b[k], b[k+1]).  Equal counts for one SHA-512 block count,
+    else equal estimated cost sum(40 + blocks)."""
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(off) - 1
+    b = np.zeros(g + 1, dtype=np.uint64)
+    _check(lib().edv_shard_split(off.ctypes.data if n > 0 else None, max(n, 0), g, b.ctypes.data))
+    return b
+
+
+class PinnedBuffer:
+    """Page-locked host memory (edv_host_alloc): batches packed here reach the
+    device by DMA without the library's staging copy.  `.array` is a uint8 view."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        _check(lib().edv_host_alloc(nbytes, ctypes.byref(p)))
+        self.ptr, self.nbytes = p.value, nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(nbytes, 1)).from_address(p.value))[:nbytes]
+
+    def view(self, dtype, offset: int = 0, count: int = -1):
+        return np.frombuffer(self.array, dtype=dtype, count=count, offset=offset)
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            lib().edv_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def pipeline_sync(device: int = 0):

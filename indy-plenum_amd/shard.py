@@ -1,17 +1,59 @@
 """Multi-GPU sharding of a verify batch by request index.
 
-Verification has no exchange step: shard k of G gets the contiguous index range
-[k*N/G, (k+1)*N/G) and nothing crosses devices until the per-request accept
-bytes are gathered back into request order (host memcpy in edv_verify_batch;
-an all-gather over torch.distributed -- RCCL over xGMI on the GPU box, gloo in
-the CPU tests -- in the one-process-per-GPU layout bench.py uses).
+Verification has no exchange step: shard k of G gets a contiguous index range
+and nothing crosses devices until the per-request accept bytes are gathered
+back into request order (host memcpy in edv_verify_batch; an all-gather over
+torch.distributed -- RCCL over xGMI -- in the one-process-per-GPU layout
+bench.py uses, which lives in bench.py, not in this package).
+
+Two splits:
+  shard_range   equal counts, [k*N/G, (k+1)*N/G)   (C2/C3: one message length)
+  shard_bounds  the split edv_verify_batch applies (include/edv.h
+                edv_shard_split): equal counts when every message has the same
+                SHA-512 block count, else equal estimated cost, the sum over a
+                shard of (VERIFY_BLOCKS + SHA-512 blocks of R||A||M)  (C4)
 """
 import numpy as np
 
+# fixed per-verify work in SHA-512-block units: W(m) = 217,600 + 5,500 * blocks
+# INT32 ops, 217,600 / 5,500 ~ 40
+VERIFY_BLOCKS = 40
+
 
 def shard_range(n_total: int, world: int, rank: int):
-    """Contiguous [lo, hi) of request indices for `rank` (same split as edv_verify_batch)."""
+    """Contiguous [lo, hi) of request indices for `rank`, equal counts."""
     return n_total * rank // world, n_total * (rank + 1) // world
+
+
+def sha512_blocks(offsets):
+    """SHA-512 compressions of R || A || M per request (64-byte prefix + padding)."""
+    off = np.asarray(offsets, dtype=np.uint64)
+    lens = (off[1:] - off[:-1]).astype(np.int64)
+    return (64 + lens + 17 + 127) // 128
+
+
+def shard_bounds(offsets, g: int):
+    """g+1 bounds of the split edv_verify_batch uses (numpy restatement of
+    edv_shard_split, checked against it in tests/test_shard_cpu.py)."""
+    off = np.asarray(offsets, dtype=np.uint64)
+    n = len(off) - 1
+    b = np.zeros(g + 1, dtype=np.int64)
+    b[g] = n
+    if n <= 0:
+        return np.zeros(g + 1, dtype=np.int64)
+    blocks = sha512_blocks(off)
+    if np.all(blocks == blocks[0]):
+        for k in range(1, g):
+            b[k] = n * k // g
+        return b
+    w = VERIFY_BLOCKS + blocks
+    pre = np.concatenate([[0], np.cumsum(w)])  # pre[i] = cost of requests [0, i)
+    total = int(pre[-1])
+    for k in range(1, g):
+        # first i (0 <= i < n) with pre[i] * g >= total * k, else n
+        i = int(np.searchsorted(pre[:n] * g, total * k, side="left"))
+        b[k] = min(i, n)
+    return b
 
 
 def slice_batch(sigs, pks, msgs, off, lo, hi):
@@ -20,26 +62,3 @@ def slice_batch(sigs, pks, msgs, off, lo, hi):
     m0, m1 = int(o[0]), int(o[-1])
     return (sigs[64 * lo:64 * hi], pks[32 * lo:32 * hi], msgs[m0:m1 + 64] if m1 + 64 <= len(msgs) else
             np.concatenate([msgs[m0:m1], np.zeros(64, np.uint8)]), o - np.uint64(m0))
-
-
-def gather_accept(dist, local_accept, n_total: int, device=None):
-    """All-gather every rank's accept bytes back into request order -> np.uint8[n_total].
-
-    `dist` is torch.distributed (initialised); shards may differ by one in size,
-    so each rank pads to the largest shard before the all-gather.
-    """
-    import torch
-    world, rank = dist.get_world_size(), dist.get_rank()
-    sizes = [shard_range(n_total, world, r) for r in range(world)]
-    mx = max(hi - lo for lo, hi in sizes)
-    buf = np.zeros(mx, dtype=np.uint8)
-    buf[:len(local_accept)] = local_accept
-    t = torch.from_numpy(buf)
-    if device is not None:
-        t = t.to(device)
-    outs = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(outs, t)
-    full = np.zeros(n_total, dtype=np.uint8)
-    for (lo, hi), o in zip(sizes, outs):
-        full[lo:hi] = o.cpu().numpy()[:hi - lo]
-    return full

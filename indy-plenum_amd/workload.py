@@ -57,11 +57,26 @@ def nym_messages(n, seed=0x5EED2025, start=0, msg_len=256, var_range=None):
     return msgs, off
 
 
-class DeviceBatch:
-    """A signed batch resident on one device: seeds -> (pks, sigs) signed on the GPU."""
+def damage_positions(start, n, every):
+    """Request indices i in [start, start + n) with i % every == every // 2 (a
+    deterministic invalid set, ~1/every of the requests), relative to start."""
+    if not every:
+        return np.zeros(0, dtype=np.int64)
+    first = (every // 2 - start) % every
+    return np.arange(first, n, every, dtype=np.int64)
 
-    def __init__(self, n, device=0, seed=0x5EED2025, start=0, msg_len=256, var_range=None):
+
+class DeviceBatch:
+    """A signed batch resident on one device: seeds -> (pks, sigs) signed on the GPU.
+
+    damage_every=k corrupts the signatures of requests i % k == k // 2 (global
+    index i = start + j), cycling over four kinds of damage (R bit flip, S + L
+    malleation, message byte, key bit), so the expected verdicts are known by
+    construction: `expected()`."""
+
+    def __init__(self, n, device=0, seed=0x5EED2025, start=0, msg_len=256, var_range=None, damage_every=0):
         self.n, self.device = n, device
+        self.start = start
         msgs, off = nym_messages(n, seed, start, msg_len, var_range)
         seeds = np.random.default_rng([seed, start, 7]).integers(0, 256, size=32 * n, dtype=np.uint8)
         self.host_msgs, self.host_off = msgs, off
@@ -76,17 +91,48 @@ class DeviceBatch:
         self.d_accept = edv.DeviceBuffer(n, device)
         edv.sign_device(d_seeds.ptr, self.d_msgs.ptr, self.d_off.ptr, n, self.d_pks.ptr, self.d_sigs.ptr, device)
         d_seeds.free()
-        # one SHA-512 block count for the whole batch: no length buckets needed
-        edv.set_length_buckets(device, 0 if var_range is None else 2)
+        # one SHA-512 block count for the whole batch: no length buckets needed (a
+        # per-call hint; the device-wide mode stays untouched)
+        self.flags = edv.FLAG_UNIFORM_LENGTH if var_range is None else 0
+        self.bad = damage_positions(start, n, damage_every)
+        if self.bad.size:
+            self._damage()
+
+    def _damage(self):
+        L = 2**252 + 27742317777372353535851937790883648493
+        sigs = self.d_sigs.download(64 * self.n).copy()
+        pks = self.d_pks.download(32 * self.n).copy()
+        msgs = self.host_msgs.copy()
+        for k, i in enumerate(self.bad.tolist()):
+            kind = (self.start + i) % 4
+            if kind == 0:
+                sigs[64 * i + 5] ^= 0x10                                    # R bit
+            elif kind == 1:
+                s = int.from_bytes(sigs[64 * i + 32:64 * i + 64].tobytes(), "little") + L
+                sigs[64 * i + 32:64 * i + 64] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)  # S + L
+            elif kind == 2:
+                msgs[int(self.host_off[i]) + 3] ^= 0x01                     # message byte
+            else:
+                pks[32 * i + 9] ^= 0x04                                     # key bit
+        self.d_sigs.upload(sigs)
+        self.d_pks.upload(pks)
+        self.host_msgs = msgs
+        self.d_msgs.upload(msgs)
+
+    def expected(self):
+        """The verdict bytes this batch must produce (1 except at the damaged positions)."""
+        e = np.ones(self.n, dtype=np.uint8)
+        e[self.bad] = 0
+        return e
 
     def verify(self, stream=None):
         edv.verify_device(self.d_sigs.ptr, self.d_pks.ptr, self.d_msgs.ptr, self.d_off.ptr, self.n,
-                          self.d_accept.ptr, self.device, stream=stream)
+                          self.d_accept.ptr, self.device, stream=stream, flags=self.flags)
 
     def submit(self):
         """Pipelined verify (edv_verify_batch_dev_pipelined); results after edv.pipeline_sync."""
         edv.verify_device_pipelined(self.d_sigs.ptr, self.d_pks.ptr, self.d_msgs.ptr, self.d_off.ptr, self.n,
-                                    self.d_accept.ptr, self.device)
+                                    self.d_accept.ptr, self.device, flags=self.flags)
 
     def accept(self):
         return self.d_accept.download(self.n)

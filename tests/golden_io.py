@@ -52,3 +52,31 @@ def load_serializer_golden():
     """Reference SigningSerializer outputs: [{"msg", "ignore", "ser"}] (make_serializer_golden.py)."""
     with open(os.path.join(GOLDEN, "serializer_golden.json")) as f:
         return json.load(f)["cases"]
+
+
+def load_sign_golden():
+    """libsodium signing vectors (make_sign_golden.py): list of (seed, msg, pk, sig)."""
+    with open(os.path.join(GOLDEN, "sign_golden.bin"), "rb") as f:
+        data = f.read()
+    assert data[:8] == b"EDVSIGN1"
+    (count,) = struct.unpack_from("<I", data, 8)
+    pos, out = 12, []
+    for _ in range(count):
+        (mlen,) = struct.unpack_from("<I", data, pos)
+        pos += 4
+        seed, pk, sig = data[pos:pos + 32], data[pos + 32:pos + 64], data[pos + 64:pos + 128]
+        msg = data[pos + 128:pos + 128 + mlen]
+        pos += 128 + mlen
+        out.append((seed, msg, pk, sig))
+    assert pos == len(data)
+    return out
+
+
+def pack_sign_batch(recs):
+    """(seeds, msgs, offsets) of signing vectors in the edv_sign_batch_dev layout."""
+    import numpy as np
+    seeds = b"".join(r[0] for r in recs)
+    msgs = b"".join(r[1] for r in recs)
+    off = np.zeros(len(recs) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(r[1]) for r in recs])
+    return seeds, msgs, off

@@ -50,3 +50,15 @@ def test_gpu_batch_equals_oracle_sequential(seed, monkeypatch):
     got = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in got]
     assert got == want
     assert sum(1 for o in want if o[0] == "ok") > 100
+
+
+def test_gpu_whole_batch_native_path(monkeypatch):
+    """CoreAuthNr.authenticate_batch through _edvhost.auth_core_batch (native
+    prep, edv_verify_batch called from C++ with the GIL released) on the real
+    GPU, against the sequential reference chain on the oracle."""
+    auth, reqs = H.make_requests(3000, seed=41)
+    want = _sequential_on_oracle(lambda: [H.outcome(lambda r=r: auth.authenticate(r)) for r in reqs], monkeypatch)
+    assert edv.native_batch_enabled()     # the genuine entry point is back in place
+    got = auth.authenticate_batch(reqs)
+    got = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in got]
+    assert got == want

@@ -1,0 +1,191 @@
+"""GPU tests of the host runtime around the kernels (include/edv.h):
+
+* f-4 signer parity: edv_sign_batch_dev == libsodium, byte for byte;
+* scratch ordering across caller streams (two batches in flight on two
+  streams at once must each get their own verdicts);
+* the host path: pinned (edv_host_alloc) and pageable inputs, sub-batches over
+  the four host-path streams, chunk seams;
+* the multi-device path (one host thread per device, edv_shard_split) on
+  EDV_VIRTUAL_DEVICES logical devices, against libsodium's committed bitmask
+  (C3 split by request index) and the checker (C4 cost-balanced split);
+* bench.py's C3 mode end to end on a bounded total.
+Bit-exact accept/reject is the bar everywhere.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import golden_io
+import oracle_lib as orc
+from indy_plenum_amd import edv
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_present():
+    assert edv.device_count() >= 1, "no gfx950 device visible: the GPU suite must run on the MI355X box"
+
+
+def checker(sigs, pks, msgs, off):
+    if orc.sodium_batch() is not None:
+        return orc.sodium_verify_batch(sigs, pks, msgs, off, 16)
+    return np.frombuffer(orc.verify_batch(sigs.tobytes(), pks.tobytes(), msgs.tobytes(), off, len(off) - 1, 16),
+                         dtype=np.uint8)
+
+
+def test_sign_batch_dev_matches_libsodium():
+    vec = golden_io.load_sign_golden()
+    seeds, msgs, off = golden_io.pack_sign_batch(vec)
+    pks, sigs = edv.sign_arrays(seeds, msgs, off)
+    bad = [i for i, r in enumerate(vec) if pks[32 * i:32 * i + 32].tobytes() != r[2]
+           or sigs[64 * i:64 * i + 64].tobytes() != r[3]]
+    assert bad == []
+    # and what the signer made verifies on the GPU verifier
+    acc = edv.verify_arrays(sigs, pks, np.frombuffer(msgs + b"\0" * 16, np.uint8), off)
+    assert acc.all()
+
+
+def _upload(*arrays):
+    bufs = []
+    for a in arrays:
+        b = edv.DeviceBuffer(a.nbytes + 64)
+        b.upload(a)
+        bufs.append(b)
+    return bufs
+
+
+def test_two_caller_streams_do_not_share_scratch():
+    """launches on different caller streams are ordered on the
+    library's scratch (st_done event), so two batches enqueued back to back on
+    two streams, without any sync between them, both come out right."""
+    import torch
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    a = orc.corpus(0x5C1, 0, 20000, mode=0, invalid_permille=300)
+    b = orc.corpus(0x5C2, 0, 30000, mode=1, invalid_permille=100)
+    want_a, want_b = checker(*a), checker(*b)
+    ba, bb = _upload(*a), _upload(*b)
+    acc_a, acc_b = edv.DeviceBuffer(20000), edv.DeviceBuffer(30000)
+    for _ in range(3):
+        edv.verify_device(ba[0].ptr, ba[1].ptr, ba[2].ptr, ba[3].ptr, 20000, acc_a.ptr, stream=s1.cuda_stream)
+        edv.verify_device(bb[0].ptr, bb[1].ptr, bb[2].ptr, bb[3].ptr, 30000, acc_b.ptr, stream=s2.cuda_stream)
+        edv.verify_device(ba[0].ptr, ba[1].ptr, ba[2].ptr, ba[3].ptr, 20000, acc_a.ptr, stream=s1.cuda_stream,
+                          flags=edv.FLAG_UNIFORM_LENGTH)
+        s1.synchronize()
+        s2.synchronize()
+        assert np.array_equal(acc_a.download(20000), want_a)
+        assert np.array_equal(acc_b.download(30000), want_b)
+
+
+def test_device_entry_points_reject_misaligned_pointers():
+    sigs, pks, msgs, off = orc.corpus(0xA1, 0, 64, mode=0, invalid_permille=0)
+    bufs = _upload(sigs, pks, msgs, off)
+    acc = edv.DeviceBuffer(64)
+    with pytest.raises(edv.EdvError):
+        edv.verify_device(bufs[0].ptr + 4, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, 64, acc.ptr)
+    with pytest.raises(edv.EdvError):
+        edv.verify_device(bufs[0].ptr, bufs[1].ptr + 8, bufs[2].ptr, bufs[3].ptr, 64, acc.ptr)
+    # an unaligned message base is fine (messages are read as aligned words):
+    # d_msgs one byte in, msg_base = 1, so message i is still at ptr + off[i]
+    edv.verify_device(bufs[0].ptr, bufs[1].ptr, bufs[2].ptr + 1, bufs[3].ptr, 64, acc.ptr, msg_base=1)
+    assert acc.download(64).all()
+
+
+@pytest.mark.parametrize("n", [1, 255, 4097, 65536 + 77])
+def test_host_path_pinned_and_pageable(n):
+    sigs, pks, msgs, off = orc.corpus(0x9E + n, 0, n, mode=n % 2, invalid_permille=150)
+    want = checker(sigs, pks, msgs, off)
+    assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off), want)
+    # the same batch from page-locked memory: direct DMA, no staging copy
+    parts = [sigs, pks, off.view(np.uint8), msgs]
+    pb = edv.PinnedBuffer(sum(p.nbytes for p in parts) + 4 * 64 + n)
+    pos, views = 0, []
+    for p in parts:
+        v = pb.array[pos:pos + p.nbytes]
+        v[:] = p
+        views.append(v)
+        pos += (p.nbytes + 63) // 64 * 64
+    acc = pb.array[pos:pos + n]
+    edv._check(edv.lib().edv_verify_batch(views[0].ctypes.data, views[1].ctypes.data, views[3].ctypes.data,
+                                          views[2].ctypes.data, n, acc.ctypes.data, 0))
+    assert np.array_equal(acc, want)
+    pb.free()
+
+
+def test_host_path_chunk_seams_with_sub_batches():
+    """Small chunks: the host path's sub-batches then span several chunk-sized
+    scratch regions per stream (and one stream when the chunk is tiny)."""
+    sigs, pks, msgs, off = orc.corpus(0xC5EA, 0, 9000, mode=1, invalid_permille=200)
+    want = checker(sigs, pks, msgs, off)
+    try:
+        for chunk in (256, 1024, 4096, 8192):
+            edv.set_chunk(0, chunk)
+            assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off), want), chunk
+    finally:
+        edv.set_chunk(0, 0)
+
+
+_VIRTUAL = r"""
+import json, os, sys
+import numpy as np
+sys.path.insert(0, os.environ["ROOT"]); sys.path.insert(0, os.path.join(os.environ["ROOT"], "tests"))
+import oracle_lib as orc
+from indy_plenum_amd import edv, shard
+out = {"devices": edv.device_count()}
+meta = json.load(open(os.path.join(os.environ["ROOT"], "tests", "golden", "corpus_bitmask.json")))
+cfg = meta["corpora"]["c2_256B"]
+n = 262144
+sigs, pks, msgs, off = orc.corpus(cfg["seed"], 0, n, cfg["mode"], cfg["invalid_permille"])
+bits = np.fromfile(os.path.join(os.environ["ROOT"], "tests", "golden", "corpus_c2_256B.bits"), np.uint8)
+want = np.unpackbits(bits[:n // 8], bitorder="little")
+got = edv.verify_arrays(sigs, pks, msgs, off)            # all logical devices, split by index
+out["c3_split_equal"] = bool(np.array_equal(got, want))
+out["c3_bounds"] = edv.shard_split(off, out["devices"]).tolist()
+got2 = edv.verify_arrays(sigs, pks, msgs, off, device_mask=0b0101)   # a subset of the devices
+out["subset_equal"] = bool(np.array_equal(got2, want))
+s4, p4, m4, o4 = orc.corpus(0xC4C4, 0, 30000, mode=1, invalid_permille=50)
+w4 = np.frombuffer(orc.verify_batch(s4.tobytes(), p4.tobytes(), m4.tobytes(), o4, 30000, 16), np.uint8)
+out["c4_equal"] = bool(np.array_equal(edv.verify_arrays(s4, p4, m4, o4), w4))
+out["c4_bounds"] = edv.shard_split(o4, out["devices"]).tolist()
+out["c4_bounds_restated"] = shard.shard_bounds(o4, out["devices"]).tolist()
+try:
+    edv.verify_arrays(s4, p4, m4, o4, device_mask=1 << 20)
+    out["bad_mask"] = "no error"
+except edv.EdvUnavailable as ex:
+    out["bad_mask"] = "EdvUnavailable"
+print(json.dumps(out))
+"""
+
+
+def test_multi_device_path_on_virtual_devices():
+    """edv_verify_batch with four logical devices (EDV_VIRTUAL_DEVICES=4 on this
+    one-GPU box): one host thread and context per device, shards by index (C2
+    lengths: equal counts) checked against libsodium's committed verdict bitmask,
+    and by estimated cost (C4 lengths) against the checker."""
+    env = dict(os.environ, EDV_VIRTUAL_DEVICES="4", ROOT=ROOT)
+    r = subprocess.run([sys.executable, "-c", _VIRTUAL], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["devices"] == 4
+    assert out["c3_split_equal"] and out["subset_equal"] and out["c4_equal"]
+    assert out["c3_bounds"] == [0, 65536, 131072, 196608, 262144]
+    assert out["c4_bounds"] == out["c4_bounds_restated"]
+    assert out["bad_mask"] == "EdvUnavailable"
+
+
+def test_bench_c3_mode_bounded():
+    """bench.py --total (C3 split by request index, 5 % damaged at known
+    positions, accept bytes checked) on a bounded total."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--total", "524288", "--steps", "2",
+                        "--reps", "2", "--warmup", "1", "--warmup-seconds", "0", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["verdicts_as_expected"] is True
+    assert line["config"]["workload"].startswith("C3")
+    assert line["value"] > 1e6

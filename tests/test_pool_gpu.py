@@ -1,0 +1,44 @@
+"""Config C5 / row f-2 on the GPU: the 4-node pool harness (Alpha..Delta,
+indy-plenum_amd/pool.py) under a client flood with the REAL gfx950 verifier
+behind ReqAuthenticator.authenticate_batch (one device call per prod) and GPU
+request digests, against the reference's message flow run on the CPU (one
+verifySignature per message, the oracle in place of libsodium, hashlib
+digests).  Every node must order the same valid set and NACK the same requests.
+
+Reference flow: plenum/server/node.py:1553-1622 (PROPAGATE validation),
+:1646-1786 (client REQUEST), :2575-2599 (verifySignature); pool fixture
+plenum/test/conftest.py:847-871 (txnPoolNodeSet, 4 nodes in one process).
+"""
+import pytest
+
+import test_authn_host as H
+from test_pool_cpu import factory, flood
+from indy_plenum_amd import digest, edv
+from indy_plenum_amd.pool import Pool, cpu_digests
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(signers, reqs, valid, batched, digest_fn):
+    pool = Pool(factory(signers), n=4, batched=batched, digest_fn=digest_fn, client_quota=50, max_batch=40)
+    pool.submit(reqs)
+    wall = pool.run(len(valid))
+    st = pool.stats(wall, len(valid))
+    st["ordered_keys"] = [sorted(nd.ordered_keys) for nd in pool.nodes.values()]
+    return st
+
+
+def test_pool_c5_gpu_batched_equals_reference_flow(monkeypatch):
+    assert edv.device_count() >= 1
+    signers, reqs, valid = flood(n_valid=400, n_bad_sig=40, n_unknown=20, seed=55)
+    with monkeypatch.context() as m:
+        m.setattr(edv, "open_batch", H.oracle_open_batch)
+        ref = _run(signers, reqs, valid, batched=False, digest_fn=cpu_digests)
+    gpu = _run(signers, reqs, valid, batched=True, digest_fn=digest.request_digests)
+    assert gpu["ordered_per_node"] == ref["ordered_per_node"] == [len(valid)] * 4
+    assert gpu["nacks_per_node"] == ref["nacks_per_node"] == [len(reqs) - len(valid)] * 4
+    assert gpu["bad_propagates"] == ref["bad_propagates"] == 0
+    assert gpu["ordered_keys"] == ref["ordered_keys"]
+    assert set(gpu["ordered_keys"][0]) == set(cpu_digests(valid))
+    assert gpu["verifies"] == ref["verifies"] == 4 * len(reqs) + 4 * 3 * len(valid)
+    assert gpu["auth_calls"] < ref["auth_calls"] / 10    # one authenticate_batch per prod

@@ -1,17 +1,29 @@
-"""Summarise rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE, one pass each) into
-per-kernel HBM bytes per launch, with the gfx950 correction of
-MI355X_MICROARCH.md "HBM": FETCH_SIZE reports half the bytes of wide coalesced
-reads, so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact (x 1024).
-Infinity-Cache (MALL) hits are counted by these counters, not excluded.
+"""Summarise rocprofv3 --pmc passes (one counter group per pass, each pass its
+own run over bench.py) into per-kernel averages per launch, plus the derived
+HBM and VALU figures bench.py reports in `roofline`.
 
-  python tools/pmc_summary.py <pmc_dir_fetch> <pmc_dir_write> [out.json]
+  python tools/pmc_summary.py <pmc_root_dir> [out.json]
+
+<pmc_root_dir> holds one sub-directory per pass (p1, p2, ...), each with the
+run_counter_collection.csv rocprofv3 wrote.
+
+HBM (MI355X_MICROARCH.md "HBM"): on gfx950 FETCH_SIZE reports half the bytes of
+wide coalesced reads, so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact
+(x 1024).  Infinity-Cache (MALL) hits are counted by these counters, not
+excluded, so the figure is an upper bound on DRAM traffic.
+
+VALU: SQ_INSTS_VALU counts wave-instructions (one per wave per VALU
+instruction); SQ_ACTIVE_INST_VALU counts them in quad-cycles; GRBM_GUI_ACTIVE
+is summed over the 8 XCDs (MI355X_MICROARCH.md "DVFS give-back"), so the
+kernel's GPU-busy cycles are GRBM_GUI_ACTIVE / 8.
 
 The summary records the SHA-256 of the kernel sources it was measured on
-(bench.kernel_source_hash); bench.py reports it as roofline.traffic only while
-the sources still hash the same.
+(bench.kernel_source_hash); bench.py reports its figures only while the
+sources still hash the same.
 """
 import collections
 import csv
+import glob
 import json
 import os
 import sys
@@ -19,35 +31,60 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import kernel_source_hash  # noqa: E402
 
+N_SIMD = 256 * 4
 
-def per_kernel(d, counter):
-    acc = collections.defaultdict(list)
-    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
-        if r["Counter_Name"] != counter:
-            continue
-        name = r["Kernel_Name"]
-        short = name.replace("(anonymous namespace)::", "").split("(")[0]
-        acc[short].append(float(r["Counter_Value"]))
-    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
+
+def short(name):
+    return name.replace("(anonymous namespace)::", "").split("(")[0]
+
+
+def collect(root):
+    """-> {kernel: {counter: [values per launch]}}, {kernel: grid sizes}"""
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    grid = collections.defaultdict(set)
+    for f in sorted(glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), recursive=True)):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            grid[k].add(int(r["Grid_Size"]))
+    return acc, grid
+
+
+def summarise(root):
+    acc, grid = collect(root)
+    out = {"source": "rocprofv3 --pmc, one counter group per pass, over bench.py --steps 6 --warmup 2",
+           "correction": "read_bytes = 2 * FETCH_SIZE_KB * 1024 (gfx950), write_bytes = WRITE_SIZE_KB * 1024; "
+                         "MALL (Infinity Cache) hits are included",
+           "kernel_source_sha256": kernel_source_hash(),
+           "kernels": {}}
+    for k, cs in sorted(acc.items()):
+        avg = {c: sum(v) / len(v) for c, v in cs.items()}
+        d = {"launches": max(len(v) for v in cs.values()), "grid_sizes": sorted(grid[k]), "counters": avg}
+        if "FETCH_SIZE" in avg or "WRITE_SIZE" in avg:
+            d["read_bytes"] = 2 * avg.get("FETCH_SIZE", 0.0) * 1024
+            d["write_bytes"] = avg.get("WRITE_SIZE", 0.0) * 1024
+            d["hbm_bytes_per_launch"] = d["read_bytes"] + d["write_bytes"]
+        if "SQ_INSTS_VALU" in avg and avg.get("SQ_WAVES"):
+            d["valu_insts_per_wave"] = avg["SQ_INSTS_VALU"] / avg["SQ_WAVES"]
+            d["salu_insts_per_wave"] = avg.get("SQ_INSTS_SALU", 0.0) / avg["SQ_WAVES"]
+            d["vmem_insts_per_wave"] = avg.get("SQ_INSTS_VMEM", 0.0) / avg["SQ_WAVES"]
+        if "SQ_ACTIVE_INST_VALU" in avg and "GRBM_GUI_ACTIVE" in avg:
+            busy = avg["GRBM_GUI_ACTIVE"] / 8.0  # GPU-busy cycles of the kernel
+            d["gpu_busy_cycles"] = busy
+            # fraction of all SIMD cycles in which a VALU instruction was issuing (quad-cycle units)
+            d["valu_busy"] = 4.0 * avg["SQ_ACTIVE_INST_VALU"] / (busy * N_SIMD)
+        if "SQ_WAVE_CYCLES" in avg:
+            wc = avg["SQ_WAVE_CYCLES"]
+            d["wave_cycle_split"] = {c: avg.get(c, 0.0) / wc for c in
+                                     ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY")}
+        out["kernels"][k] = d
+    return out
 
 
 def main():
-    fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
-    write = per_kernel(sys.argv[2], "WRITE_SIZE")
-    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py",
-           "correction": "read_bytes = 2 * FETCH_SIZE_KB * 1024 (gfx950), write_bytes = WRITE_SIZE_KB * 1024",
-           "kernel_source_sha256": kernel_source_hash(),
-           "bench_args": "--steps 6 --warmup 20 --no-cpu-baseline (batch 65536 x 256 B)",
-           "kernels": {}}
-    for k in sorted(set(fetch) | set(write)):
-        f, nf = fetch.get(k, (0.0, 0))
-        w, nw = write.get(k, (0.0, 0))
-        out["kernels"][k] = {"fetch_size_kb": f, "write_size_kb": w, "launches": max(nf, nw),
-                             "read_bytes": 2 * f * 1024, "write_bytes": w * 1024,
-                             "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024}
-    s = json.dumps(out, indent=1)
-    if len(sys.argv) > 3:
-        open(sys.argv[3], "w").write(s + "\n")
+    s = json.dumps(summarise(sys.argv[1]), indent=1)
+    if len(sys.argv) > 2:
+        open(sys.argv[2], "w").write(s + "\n")
     print(s)
 
 
