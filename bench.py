@@ -274,12 +274,21 @@ def e2e_leg(batch, device_value, reps=5):
 def node_path_leg(n=65536, reps=3):
     """f-1: CoreAuthNr.authenticate_batch over n C1-shaped requests on this GPU
     (native host prep, one verify call, replay)."""
+    from indy_plenum_amd import _edvhost
+    from indy_plenum_amd.req_authenticator import ReqAuthenticator
     auth, reqs = c1_requests(n, seed=0xF1)
     res = auth.authenticate_batch(reqs)
     assert all(x == [r["identifier"]] for x, r in zip(res, reqs))
     t = median_time(lambda: auth.authenticate_batch(reqs), reps)
-    return {"what": "CoreAuthNr.authenticate_batch, %d NYM requests, 1 GPU, median of %d" % (n, reps),
-            "requests_per_s": n / t, "ms": 1e3 * t}
+    phases = _edvhost.last_phases()
+    ra = ReqAuthenticator()
+    ra.register_authenticator(auth)
+    assert all(x == {r["identifier"]} for x, r in zip(ra.authenticate_batch(reqs), reqs))
+    t_ra = median_time(lambda: ra.authenticate_batch(reqs), reps)
+    return {"what": "CoreAuthNr.authenticate_batch, %d NYM requests (~150 B signing bytes), 1 GPU, median of %d; "
+                    "native host prep on %d threads" % (n, reps, edv.PREP_THREADS),
+            "requests_per_s": n / t, "ms": 1e3 * t, "phases_last_call_s": phases,
+            "req_authenticator_requests_per_s": n / t_ra}
 
 
 def main():

@@ -26,6 +26,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <thread>
 #include <vector>
@@ -135,12 +136,64 @@ bool text_arg(PyObject* o, const uint8_t** p, Py_ssize_t* n, bool* is_str) {
   return false;
 }
 
+// b58_decode for str text of at most 128 characters, into out[cap], with no
+// heap allocation (the decode threads of auth_core_batch): same semantics as
+// b58_decode(s, n, true, ...); returns the byte length, or -1 if the text is
+// not handled here (invalid character, too long, result longer than cap).
+int b58_decode_small(const uint8_t* s, size_t n, uint8_t* out, size_t cap) {
+  while (n && str_space(s[n - 1])) n--;
+  if (n > 128) return -1;
+  size_t ones = 0;
+  while (ones < n && s[ones] == '1') ones++;
+  uint64_t limb[12];  // little-endian 64-bit limbs; 128 digits < 2^751
+  size_t nl = 0;
+  size_t i = ones;
+  while (i < n) {  // ten base-58 digits (58^10 < 2^59) per multiply-add pass
+    uint64_t chunk = 0, mul = 1;
+    for (int k = 0; k < 10 && i < n; k++, i++) {
+      const int d = g_index[s[i]];
+      if (d < 0) return -1;
+      chunk = chunk * 58u + uint64_t(d);
+      mul *= 58u;
+    }
+    uint64_t carry = chunk;
+    for (size_t l = 0; l < nl; l++) {
+      const unsigned __int128 v = (unsigned __int128)limb[l] * mul + carry;
+      limb[l] = uint64_t(v);
+      carry = uint64_t(v >> 64);
+    }
+    if (carry) limb[nl++] = carry;
+  }
+  size_t len = ones;
+  bool lead = true;
+  uint8_t tmp[100];
+  size_t tl = 0;
+  for (size_t k = nl; k-- > 0;)
+    for (int b = 7; b >= 0; b--) {
+      const uint8_t c = uint8_t(limb[k] >> (8 * b));
+      if (lead && c == 0) continue;
+      lead = false;
+      tmp[tl++] = c;
+    }
+  len += tl;
+  if (len > cap) return -1;
+  memset(out, 0, ones);
+  memcpy(out + ones, tmp, tl);
+  return int(len);
+}
+
 PyObject* py_b58decode(PyObject*, PyObject* arg) {
   const uint8_t* p;
   Py_ssize_t n;
   bool is_str;
   std::string out;
-  if (!text_arg(arg, &p, &n, &is_str) || !b58_decode(p, size_t(n), is_str, &out)) Py_RETURN_NOTIMPLEMENTED;
+  if (!text_arg(arg, &p, &n, &is_str)) Py_RETURN_NOTIMPLEMENTED;
+  if (is_str && n <= 128) {  // the allocation-free decoder the batch path uses
+    uint8_t buf[128];
+    const int len = b58_decode_small(p, size_t(n), buf, sizeof buf);
+    if (len >= 0) return PyBytes_FromStringAndSize(reinterpret_cast<const char*>(buf), len);
+  }
+  if (!b58_decode(p, size_t(n), is_str, &out)) Py_RETURN_NOTIMPLEMENTED;
   return PyBytes_FromStringAndSize(out.data(), Py_ssize_t(out.size()));
 }
 
@@ -183,46 +236,63 @@ int ser(PyObject* obj, int level, PyObject* ignore, std::string& out) {
   if (PyUnicode_Check(obj)) {
     r = append_str(obj, out);
   } else if (PyDict_Check(obj)) {
-    // keys (minus the top-level ignore list), sorted; str keys only here
+    // keys (minus the top-level ignore list), sorted; str keys only here.
+    // Request dicts have a handful of keys: a stack buffer and an insertion
+    // sort (no heap allocation per dict).
     struct Item {
       const char* k;  // UTF-8 of the key object ko
       size_t n;
       PyObject* ko;
       PyObject* v;
     };
-    std::vector<Item> items;
+    constexpr Py_ssize_t kStack = 16;
+    Item stack_items[kStack];
+    std::vector<Item> heap_items;
+    const Py_ssize_t cap = PyDict_GET_SIZE(obj);
+    Item* items = stack_items;
+    if (cap > kStack) {
+      heap_items.resize(size_t(cap));
+      items = heap_items.data();
+    }
+    Py_ssize_t cnt = 0;
+    const bool ign_set = ignore && PyAnySet_Check(ignore);
     PyObject *k, *v;
     Py_ssize_t pos = 0;
     while (r == 1 && PyDict_Next(obj, &pos, &k, &v)) {
       if (!PyUnicode_CheckExact(k)) { r = 0; break; }
       if (level == 0 && ignore) {
-        const int c = PySequence_Contains(ignore, k);
+        const int c = ign_set ? PySet_Contains(ignore, k) : PySequence_Contains(ignore, k);
         if (c < 0) { r = -1; break; }
         if (c) continue;
       }
       Py_ssize_t n;
       const char* u = PyUnicode_AsUTF8AndSize(k, &n);
       if (!u) { PyErr_Clear(); r = 0; break; }
+      if (cnt >= cap) { r = 0; break; }  // the dict grew under us: leave it to Python
       Py_INCREF(k);  // str() of a value may run Python code: hold keys and values
       Py_INCREF(v);
-      items.push_back(Item{u, size_t(n), k, v});
+      // insertion sort by UTF-8 bytes (== code point order == Python's str sort)
+      Py_ssize_t at = cnt++;
+      while (at > 0) {
+        const Item& p = items[at - 1];
+        const int c = memcmp(p.k, u, p.n < size_t(n) ? p.n : size_t(n));
+        if (c < 0 || (c == 0 && p.n <= size_t(n))) break;
+        items[at] = p;
+        at--;
+      }
+      items[at] = Item{u, size_t(n), k, v};
     }
     if (r == 1) {
-      // UTF-8 byte order == code point order == Python's str sort
-      std::sort(items.begin(), items.end(), [](const Item& a, const Item& b) {
-        const int c = memcmp(a.k, b.k, a.n < b.n ? a.n : b.n);
-        return c != 0 ? c < 0 : a.n < b.n;
-      });
-      for (size_t i = 0; r == 1 && i < items.size(); i++) {
+      for (Py_ssize_t i = 0; r == 1 && i < cnt; i++) {
         if (i) out.push_back('|');
         out.append(items[i].k, items[i].n);
         out.push_back(':');
         r = ser(items[i].v, level + 1, nullptr, out);
       }
     }
-    for (auto& it : items) {
-      Py_DECREF(it.ko);
-      Py_DECREF(it.v);
+    for (Py_ssize_t i = 0; i < cnt; i++) {
+      Py_DECREF(items[i].ko);
+      Py_DECREF(items[i].v);
     }
   } else if (PyList_Check(obj)) {
     const Py_ssize_t n = PyList_GET_SIZE(obj);
@@ -246,9 +316,13 @@ int ser(PyObject* obj, int level, PyObject* ignore, std::string& out) {
       PyErr_Clear();
       r = append_pystr(obj, out);
     } else {
-      char buf[32];
-      const int len = snprintf(buf, sizeof buf, "%lld", x);
-      out.append(buf, size_t(len));
+      char buf[24];
+      char* e = buf + sizeof buf;
+      char* q = e;
+      unsigned long long u = x < 0 ? 0ull - (unsigned long long)x : (unsigned long long)x;
+      do { *--q = char('0' + u % 10); u /= 10; } while (u);
+      if (x < 0) *--q = '-';
+      out.append(q, size_t(e - q));
     }
   } else if (PyLong_Check(obj) || PyFloat_Check(obj)) {
     r = append_pystr(obj, out);  // str(x): repr for floats, __str__ of int subclasses
@@ -506,11 +580,13 @@ inline bool ascii_str(PyObject* o, const uint8_t** p, size_t* n) {
 }
 
 // phase A for one request: false = not the fast path (nothing appended)
+PyObject *g_k_identifier, *g_k_signature, *g_k_verkey;  // interned key strings (module init)
+
 int collect_one(PyObject* req, PyObject* clients, PyObject* excluded, Py_ssize_t k, std::string& msgs,
                 FastItem* it) {
   if (!PyDict_CheckExact(req)) return 0;
-  PyObject* idr = PyDict_GetItemString(req, "identifier");
-  PyObject* sig = PyDict_GetItemString(req, "signature");
+  PyObject* idr = PyDict_GetItem(req, g_k_identifier);
+  PyObject* sig = PyDict_GetItem(req, g_k_signature);
   if (!idr || !sig) return 0;
   it->k = k;
   it->idr = idr;
@@ -520,7 +596,7 @@ int collect_one(PyObject* req, PyObject* clients, PyObject* excluded, Py_ssize_t
   PyObject* nym = PyDict_GetItemWithError(clients, idr);
   if (!nym) return PyErr_Occurred() ? -1 : 0;
   if (!PyDict_CheckExact(nym) || PyDict_GET_SIZE(nym) == 0) return 0;
-  PyObject* verkey = PyDict_GetItemString(nym, "verkey");
+  PyObject* verkey = PyDict_GetItem(nym, g_k_verkey);
   if (!verkey || !ascii_str(verkey, &it->vk_p, &it->vk_n)) return 0;
   it->sig_o = sig;
   it->vk_o = verkey;
@@ -544,24 +620,30 @@ int collect_one(PyObject* req, PyObject* clients, PyObject* excluded, Py_ssize_t
 
 // phase B for one item: signature -> sig64, key -> pk32; false = not the fast path
 bool decode_one(const FastItem& it, uint8_t* sig64, uint8_t* pk32) {
-  std::string s, a, b;
-  if (!b58_decode(it.sig, it.sig_n, true, &s) || s.size() != 64) return false;
-  memcpy(sig64, s.data(), 64);
-  if (it.vk_kind == 2) {
-    if (!b58_decode(it.vk_p, it.vk_n, true, &a) || a.size() != 32) return false;
-    memcpy(pk32, a.data(), 32);
-    return true;
-  }
-  if (!b58_decode(it.idr_p, it.idr_n, true, &a)) return false;
+  uint8_t a[40], b[40];
+  if (b58_decode_small(it.sig, it.sig_n, sig64, 64) != 64) return false;
+  if (it.vk_kind == 2) return b58_decode_small(it.vk_p, it.vk_n, pk32, 32) == 32;
+  const int la = b58_decode_small(it.idr_p, it.idr_n, a, sizeof a);
+  if (la < 0) return false;
   if (it.vk_kind == 0) {
-    if (a.size() != 32) return false;  // cryptonym: the identifier is the key
-    memcpy(pk32, a.data(), 32);
+    if (la != 32) return false;  // cryptonym: the identifier is the key
+    memcpy(pk32, a, 32);
     return true;
   }
-  if (!b58_decode(it.vk_p, it.vk_n, true, &b) || a.size() + b.size() != 32) return false;
-  memcpy(pk32, a.data(), a.size());
-  memcpy(pk32 + a.size(), b.data(), b.size());
+  const int lb = b58_decode_small(it.vk_p, it.vk_n, b, sizeof b);
+  if (lb < 0 || la + lb != 32) return false;
+  memcpy(pk32, a, size_t(la));
+  memcpy(pk32 + la, b, size_t(lb));
   return true;
+}
+
+double g_phase_s[4];  // seconds of the last auth_core_batch: A (GIL), B (decode), C (verify), D (output)
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+PyObject* py_last_phases(PyObject*, PyObject*) {
+  return Py_BuildValue("{s:d,s:d,s:d,s:d}", "collect_serialize_s", g_phase_s[0], "decode_pack_s", g_phase_s[1],
+                       "verify_s", g_phase_s[2], "output_s", g_phase_s[3]);
 }
 
 PyObject* py_auth_core_batch(PyObject*, PyObject* args) {
@@ -581,6 +663,7 @@ PyObject* py_auth_core_batch(PyObject*, PyObject* args) {
   std::string msgs;
   std::vector<uint64_t> moff(1, 0);
   std::vector<Py_ssize_t> slow_idx;
+  double t0 = now_s(), t1 = t0, t2 = t0;
   // phase A
   for (Py_ssize_t k = 0; k < n; k++) {
     FastItem it;
@@ -600,6 +683,9 @@ PyObject* py_auth_core_batch(PyObject*, PyObject* args) {
     }
   } hold{items};
   const size_t nf = items.size();
+  const double ta = now_s();
+  g_phase_s[0] = ta - t0;
+  t0 = t1 = t2 = ta;
   std::vector<uint8_t> good(nf, 1);
   Arena* ar = take_arena();
   // arena layout: sigs 64 nf | pks 32 nf | off 8 (nf + 1) | msgs (+64 slack) | accept nf
@@ -633,9 +719,11 @@ PyObject* py_auth_core_batch(PyObject*, PyObject* args) {
     for (auto& x : th) x.join();
     memcpy(base + o_off, moff.data(), 8 * (nf + 1));
     memset(base + o_msg + msgs.size(), 0, 64);
+    t1 = now_s();
     // phase C: one device call
     rc = verify(base, base + o_pk, base + o_msg, reinterpret_cast<const uint64_t*>(base + o_off), uint64_t(nf),
                 base + o_acc, mask);
+    t2 = now_s();
     Py_END_ALLOW_THREADS
   }
   if (rc != 0) {
@@ -679,6 +767,9 @@ PyObject* py_auth_core_batch(PyObject*, PyObject* args) {
     }
   }
   if (PyList_Sort(slow) < 0) goto fail;
+  g_phase_s[1] = t1 - t0;
+  g_phase_s[2] = t2 - t1;
+  g_phase_s[3] = now_s() - t2;
   res = Py_BuildValue("(NNN)", out, slow, rejected);
   g_arenas.push_back(ar);
   Py_DECREF(seq);
@@ -695,6 +786,7 @@ fail:
 PyMethodDef kMethods[] = {
     {"auth_core_batch", py_auth_core_batch, METH_VARARGS,
      "whole-batch CoreAuthNr fast path with the GPU verify inside: (out, slow, rejected)"},
+    {"last_phases", py_last_phases, METH_NOARGS, "phase seconds of the last auth_core_batch call"},
     {"set_host_allocator", py_set_host_allocator, METH_VARARGS,
      "page-locked arena allocator (edv_host_alloc, edv_host_free addresses)"},
     {"prep_core_batch", py_prep_core_batch, METH_VARARGS, "CoreAuthNr single-signature fast path (None = Python)"},
@@ -711,5 +803,9 @@ PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_edvhost", "native host prep for 
 
 PyMODINIT_FUNC PyInit__edvhost(void) {
   init_index();
+  g_k_identifier = PyUnicode_InternFromString("identifier");
+  g_k_signature = PyUnicode_InternFromString("signature");
+  g_k_verkey = PyUnicode_InternFromString("verkey");
+  if (!g_k_identifier || !g_k_signature || !g_k_verkey) return nullptr;
   return PyModule_Create(&kModule);
 }

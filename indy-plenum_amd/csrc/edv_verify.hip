@@ -686,10 +686,16 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
               uint64_t hi, uint8_t* accept) {
   const uint64_t n = hi - lo;
   if (n == 0) return 0;
-  int Q = c.chunk >= uint64_t(kQ) * kBlock ? kQ : 1;
-  if (const char* e = getenv("EDV_HOST_STREAMS")) {  // A/B measurement knob (1..4)
+  // A shard that fits one chunk is one sub-batch on one stream: split 2 or 4
+  // ways at 64k it measured 1.6x / 1.9x slower (tools/e2e_probe.py,
+  // profiles/r02/e2e_probe_s4.json), as a 16k sub-batch still takes a whole
+  // batch's latency at one wave per SIMD.  A larger shard alternates two
+  // streams of half-chunk sub-batches, so the H2D copy of one overlaps the
+  // kernels of the other.  EDV_HOST_STREAMS (1..4) overrides, for measurement.
+  int Q = (n > c.chunk && c.chunk >= 2 * uint64_t(kBlock)) ? 2 : 1;
+  if (const char* e = getenv("EDV_HOST_STREAMS")) {
     const int v = atoi(e);
-    if (v >= 1 && v <= Q) Q = v;
+    if (v >= 1 && v <= kQ && c.chunk >= uint64_t(v) * kBlock) Q = v;
   }
   const uint64_t pmax = c.chunk / Q;
   uint64_t P = (n + Q - 1) / Q;

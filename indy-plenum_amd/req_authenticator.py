@@ -43,28 +43,45 @@ class ReqAuthenticator:
     def authenticate_batch(self, reqs):
         n = len(reqs)
         out = [None] * n
-        idents = [set() for _ in range(n)]
+        typs = [None] * n
         alive = []  # requests still being processed (no result yet)
-        typs = []
         for k, req in enumerate(reqs):
             try:
-                typs.append(req.get(OPERATION, {}).get(TXN_TYPE))
+                typs[k] = req.get(OPERATION, {}).get(TXN_TYPE)
             except Exception as ex:  # malformed operation: authenticate() would raise the same
-                typs.append(None)
                 out[k] = ex
                 continue
             alive.append(k)
+        idents = {}  # k -> union of the identifier sets returned so far
         for authenticator in self._authenticators:
             if not alive:
                 break
-            todo = []
-            still = []
+            # is_query / is_write / is_action once per distinct type (pure predicates
+            # of the type in the reference: client_authn.py:185-193)
+            def kind(t):
+                return 0 if authenticator.is_query(t) else \
+                    (2 if authenticator.is_write(t) or authenticator.is_action(t) else 1)
+            kinds = {}
+            still, todo = [], []
             for k in alive:
-                if authenticator.is_query(typs[k]):
+                t = typs[k]
+                try:
+                    kd, cache = kinds.get(t), True
+                except TypeError:  # an unhashable type value: evaluate it directly
+                    kd, cache = None, False
+                if kd is None:
+                    try:
+                        kd = kind(t)
+                    except Exception as ex:  # what authenticate() raises for this request
+                        out[k] = ex
+                        continue
+                    if cache:
+                        kinds[t] = kd
+                if kd == 0:
                     out[k] = set()
                     continue
                 still.append(k)
-                if authenticator.is_write(typs[k]) or authenticator.is_action(typs[k]):
+                if kd == 2:
                     todo.append(k)
             alive = still
             if not todo:
@@ -73,8 +90,10 @@ class ReqAuthenticator:
                 # the reference deep-copies per authenticator (req_authenticator.py:39) so a
                 # plugin cannot alter the request; the stock batch path never mutates it
                 ro = getattr(authenticator, "batch_reads_only", None)
-                copy = (lambda r: r) if (ro is not None and ro()) else deepcopy
-                results = authenticator.authenticate_batch([copy(reqs[k]) for k in todo])
+                if ro is not None and ro():
+                    results = authenticator.authenticate_batch([reqs[k] for k in todo])
+                else:
+                    results = authenticator.authenticate_batch([deepcopy(reqs[k]) for k in todo])
             else:
                 results = []
                 for k in todo:
@@ -82,16 +101,21 @@ class ReqAuthenticator:
                         results.append(authenticator.authenticate(deepcopy(reqs[k])))
                     except Exception as ex:
                         results.append(ex)
-            failed = set()
+            failed = False
             for k, rv in zip(todo, results):
                 if isinstance(rv, BaseException):
                     out[k] = rv
-                    failed.add(k)
-                else:
-                    idents[k].update(rv or set())
-            alive = [k for k in alive if k not in failed]
+                    failed = True
+                elif rv:
+                    cur = idents.get(k)
+                    if cur is None:
+                        idents[k] = set(rv)
+                    else:
+                        cur.update(rv)
+            if failed:
+                alive = [k for k in alive if out[k] is None]
         for k in alive:
-            out[k] = idents[k] if idents[k] else NoAuthenticatorFound()
+            out[k] = idents.get(k) or NoAuthenticatorFound()
         return out
 
     @property

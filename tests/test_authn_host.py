@@ -308,3 +308,19 @@ def test_req_authenticator_query_and_no_authenticator():
         ra.authenticate({'operation': {'type': '101'}, 'identifier': IDR, 'signature': 'x'})
     res = ra.authenticate_batch([{'operation': {'type': '3'}}, {'operation': {'type': '101'}}])
     assert res[0] == set() and isinstance(res[1], NoAuthenticatorFound)
+
+
+def test_req_authenticator_batch_odd_types_equal_sequential(cpu_checker):
+    """Per-type predicate caching in ReqAuthenticator.authenticate_batch keeps the
+    sequential outcome for unhashable / missing / None types too (the reference's
+    `typ in self.query_types` raises TypeError for a list type)."""
+    sa, reqs = make_requests(60, seed=9)
+    odd = [dict(reqs[0], operation={'type': ['1']}), dict(reqs[1], operation={'type': {'a': 1}}),
+           dict(reqs[2], operation={}), dict(reqs[3], operation={'type': None}), dict(reqs[4], operation=None)]
+    ra = ReqAuthenticator()
+    ra.register_authenticator(sa)
+    allr = odd + reqs
+    seq = [outcome(lambda r=r: ra.authenticate(r)) for r in allr]
+    bat = ra.authenticate_batch(allr)
+    bat = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in bat]
+    assert bat == seq

@@ -55,6 +55,22 @@ def test_b58_random_roundtrip():
         assert api_dec(t) == py_dec(t)
 
 
+def test_b58_decoder_lengths_around_the_fast_path_limit():
+    """str inputs up to 128 characters take the allocation-free 64-bit-limb
+    decoder (also used by the batch path's decode threads), longer ones the
+    general one: both equal the restatement, including leading '1's and
+    trailing whitespace at every length."""
+    r = random.Random(17)
+    alpha = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
+    for n in list(range(0, 140)) + [200, 300]:
+        for _ in range(6):
+            t = "1" * r.randrange(0, 4) + "".join(r.choice(alpha) for _ in range(n))
+            t += r.choice(["", " ", "\t\n", "\x1f"])
+            assert _edvhost.b58decode(t) == py_dec(t), (n, t)
+    assert _edvhost.b58decode("z" * 128) == py_dec("z" * 128)
+    assert _edvhost.b58decode("1" * 128) == b"\0" * 128
+
+
 def _rand_obj(r, depth=0):
     k = r.randrange(9 if depth < 3 else 6)
     if k == 0:
