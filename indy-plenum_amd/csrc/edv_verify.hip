@@ -131,7 +131,11 @@ __device__ __forceinline__ void load_words(uint32_t* out, const uint32_t* p, int
 }
 
 // Phase 1: V2-V7, digit recoding, the per-signature A table.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 8))) void edv_prep_kernel(VerifyArgs a) {
+#ifndef EDV_PREP_WAVES
+#define EDV_PREP_WAVES 2  // minimum waves per SIMD the prep kernel's register budget must allow
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EDV_PREP_WAVES, 8))) void edv_prep_kernel(
+    VerifyArgs a) {
   const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;  // slot within the chunk
   if (j >= a.n) return;
   const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);

@@ -21,31 +21,8 @@ constexpr int kBStride = 32;                    // words per B / comb entry (30 
 EDV_HD uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
   return uint32_t(((uint64_t(hi) << 32) | lo) >> (8 * sh));
 }
-// Big-endian SHA word of message bytes [q, q+8) with the SHA-512 pad byte 0x80
-// at mlen and zeros after it.  Reads whole aligned 32-bit words: the buffer must
-// be readable up to 12 bytes past the message end.
-EDV_HD uint64_t msg_word(const uint8_t* m, uint64_t mlen, uint64_t q) {
-  const int64_t rem = int64_t(mlen) - int64_t(q);
-  const int nvalid = rem <= 0 ? 0 : (rem >= 8 ? 8 : int(rem));
-  uint32_t lo = 0, hi = 0;
-  if (nvalid > 0) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(m + q);
-    const uint32_t sh = uint32_t(a & 3);
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(a - sh);
-    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
-    lo = alignbyte(d1, d0, sh);
-    hi = alignbyte(d2, d1, sh);
-  }
-  uint64_t v = (uint64_t(hi) << 32) | lo;  // little-endian byte order
-  if (nvalid < 8) {
-    v &= (uint64_t(1) << (8 * nvalid)) - 1;
-    if (rem >= 0) v |= uint64_t(0x80) << (8 * nvalid);
-  }
-  return be64_from_le_words(uint32_t(v), uint32_t(v >> 32));
-}
-
 // N big-endian SHA words of message bytes [q, q + 8N) that lie wholly inside the
-// message: funnel-shifted aligned loads, none of msg_word's clamp/pad selects.
+// message: funnel-shifted aligned loads, none of msg_words_tail's clamp/pad work.
 template <int N>
 EDV_HD void msg_words_full(uint64_t* W, const uint8_t* m, uint64_t q) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(m + q);
@@ -57,6 +34,42 @@ EDV_HD void msg_words_full(uint64_t* W, const uint8_t* m, uint64_t q) {
 #pragma unroll
   for (int t = 0; t < N; t++)
     W[t] = be64_from_le_words(alignbyte(d[2 * t + 1], d[2 * t], sh), alignbyte(d[2 * t + 2], d[2 * t + 1], sh));
+}
+
+// N big-endian SHA words of message bytes [q0, q0 + 8N) of which some (or all)
+// lie past the message end: 0x80 pad byte at mlen, zeros after it.  Branch-free:
+// every dword address is clamped to the dword holding byte mlen (readable: the
+// buffer extends 16 bytes past the message), so all 2N+1 loads issue together
+// and the block waits for memory once.  (A per-word `if (bytes remain) load`
+// compiled to a load + wait per word: ~16 serialized memory latencies in the
+// last block of every message.)
+template <int N>
+EDV_HD void msg_words_tail(uint64_t* W, const uint8_t* m, uint64_t mlen, uint64_t q0) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(m) + q0;
+  const uint32_t sh = uint32_t(a & 3);
+  const uintptr_t base = a - sh;
+  const uintptr_t last = (reinterpret_cast<uintptr_t>(m) + mlen) & ~uintptr_t(3);
+  uint32_t d[2 * N + 1];
+#pragma unroll
+  for (int t = 0; t < 2 * N + 1; t++) {
+    const uintptr_t ad = base + 4 * uintptr_t(t);
+    d[t] = *reinterpret_cast<const uint32_t*>(ad < last ? ad : last);
+  }
+  // byte masks without selects (a VCC-mask v_cndmask_b32 costs ~23 cycles on
+  // gfx950): keep(k) = low k bytes set, as two shifts of at most 32 so k = 8 works
+  const int32_t rem0 = int32_t(int64_t(mlen) - int64_t(q0));  // messages are far below 2 GiB
+#pragma unroll
+  for (int t = 0; t < N; t++) {
+    const int32_t r = rem0 - 8 * t;
+    const int32_t nv = r < 0 ? 0 : (r > 8 ? 8 : r);            // v_med3_i32
+    const int32_t nv1 = r + 1 < 0 ? 0 : (r + 1 > 8 ? 8 : r + 1);
+    const uint64_t keep = ((uint64_t(1) << (4 * nv)) << (4 * nv)) - 1;
+    const uint64_t keep1 = ((uint64_t(1) << (4 * nv1)) << (4 * nv1)) - 1;
+    uint64_t v = (uint64_t(alignbyte(d[2 * t + 2], d[2 * t + 1], sh)) << 32) | alignbyte(d[2 * t + 1], d[2 * t], sh);
+    // the 0x80 pad byte sits at byte r when 0 <= r < 8: the one byte keep1 adds to keep
+    v = (v & keep) | ((keep ^ keep1) & 0x8080808080808080ULL);
+    W[t] = be64_from_le_words(uint32_t(v), uint32_t(v >> 32));
+  }
 }
 
 // SHA-512(P || M) for a 32- or 64-byte prefix P given as little-endian words,
@@ -75,8 +88,7 @@ EDV_HD void sha512_pm(uint32_t out[16], const uint32_t* P, const uint8_t* m, uin
   if (mlen >= uint64_t(128 - PB)) {
     msg_words_full<16 - PW>(W + PW, m, 0);
   } else {
-#pragma unroll
-    for (int t = PW; t < 16; t++) W[t] = msg_word(m, mlen, uint64_t(8 * (t - PW)));
+    msg_words_tail<16 - PW>(W + PW, m, mlen, 0);
   }
   if (nb == 1) { W[14] = total >> 61; W[15] = total << 3; }
   sha512_compress(H, W);
@@ -86,8 +98,7 @@ EDV_HD void sha512_pm(uint32_t out[16], const uint32_t* P, const uint8_t* m, uin
     if (q0 + 128 <= mlen) {
       msg_words_full<16>(W, m, q0);
     } else {
-#pragma unroll
-      for (int t = 0; t < 16; t++) W[t] = msg_word(m, mlen, q0 + 8 * t);
+      msg_words_tail<16>(W, m, mlen, q0);
     }
     if (b == nb - 1) { W[14] = total >> 61; W[15] = total << 3; }
     sha512_compress(H, W);

@@ -9,12 +9,29 @@ union of identifiers, NoAuthenticatorFound.  Authenticators are applied in
 order; each batch-capable one (authenticate_batch) sees all requests still
 alive at its position in one call, i.e. one GPU launch per authenticator.
 """
+import gc
+from contextlib import contextmanager
 from copy import deepcopy
 from typing import Optional
 
 from .client_authn import ClientAuthNr
 from .constants import OPERATION, TXN_TYPE
 from .exceptions import NoAuthenticatorFound
+
+
+@contextmanager
+def gc_paused():
+    """Pause the cyclic GC while a batch makes one small container per request
+    (identifier sets, lists): at node scale the allocations otherwise trigger
+    repeated collections over every live object; the young objects are
+    collected once, after.  Re-entrant; restores the previous state."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 class ReqAuthenticator:
@@ -41,6 +58,10 @@ class ReqAuthenticator:
         return identifiers
 
     def authenticate_batch(self, reqs):
+        with gc_paused():
+            return self._authenticate_batch(reqs)
+
+    def _authenticate_batch(self, reqs):
         n = len(reqs)
         out = [None] * n
         typs = [None] * n
