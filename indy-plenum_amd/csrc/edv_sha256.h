@@ -53,24 +53,34 @@ EDV_HD void sha256_compress(uint32_t H[8], uint32_t W[16]) {
   H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
 }
 
-// Big-endian SHA-256 word of message bytes [q, q+4) with the pad byte 0x80 at
-// mlen and zeros after it.  Reads whole aligned 32-bit words: the buffer must
-// be readable up to 8 bytes past the message end.
-EDV_HD uint32_t msg_word32(const uint8_t* m, uint64_t mlen, uint64_t q) {
-  const int64_t rem = int64_t(mlen) - int64_t(q);
-  const int nvalid = rem <= 0 ? 0 : (rem >= 4 ? 4 : int(rem));
-  uint32_t v = 0;
-  if (nvalid > 0) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(m + q);
-    const uint32_t sh = uint32_t(a & 3);
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(a - sh);
-    v = uint32_t(((uint64_t(p[1]) << 32) | p[0]) >> (8 * sh));  // little-endian byte order
+// The 16 big-endian words of a 64-byte block [q0, q0 + 64) that reaches past the
+// message end (0x80 pad byte at mlen, zeros after): every dword address clamped
+// to the one holding byte mlen (the buffer is readable 8 bytes past the message),
+// so the 17 loads issue together, and the masks come from shifts, not selects
+// (msg_word32 per word compiled to a load + wait per word).
+EDV_HD void msg_words32_tail(uint32_t W[16], const uint8_t* m, uint64_t mlen, uint64_t q0) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(m) + q0;
+  const uint32_t sh = uint32_t(a & 3);
+  const uintptr_t base = a - sh;
+  const uintptr_t last = (reinterpret_cast<uintptr_t>(m) + mlen) & ~uintptr_t(3);
+  uint32_t d[17];
+#pragma unroll
+  for (int t = 0; t < 17; t++) {
+    const uintptr_t ad = base + 4 * uintptr_t(t);
+    d[t] = *reinterpret_cast<const uint32_t*>(ad < last ? ad : last);
   }
-  if (nvalid < 4) {
-    v &= nvalid == 0 ? 0u : (0xffffffffu >> (32 - 8 * nvalid));
-    if (rem >= 0) v |= 0x80u << (8 * nvalid);
+  const int32_t rem0 = int32_t(int64_t(mlen) - int64_t(q0));
+#pragma unroll
+  for (int t = 0; t < 16; t++) {
+    const int32_t r = rem0 - 4 * t;
+    const int32_t nv = r < 0 ? 0 : (r > 4 ? 4 : r);
+    const int32_t nv1 = r + 1 < 0 ? 0 : (r + 1 > 4 ? 4 : r + 1);
+    const uint32_t keep = ((1u << (4 * nv)) << (4 * nv)) - 1u;   // low nv bytes (nv = 4: all)
+    const uint32_t keep1 = ((1u << (4 * nv1)) << (4 * nv1)) - 1u;
+    uint32_t v = uint32_t(((uint64_t(d[t + 1]) << 32) | d[t]) >> (8 * sh));  // little-endian byte order
+    v = (v & keep) | ((keep ^ keep1) & 0x80808080u);
+    W[t] = bswap32(v);
   }
-  return bswap32(v);
 }
 
 // SHA-256(M) -> 8 big-endian-order words of the digest, stored as bytes by the caller.
@@ -94,8 +104,7 @@ EDV_HD void sha256_msg(uint32_t out[8], const uint8_t* m, uint64_t mlen) {
 #pragma unroll
       for (int t = 0; t < 16; t++) W[t] = bswap32(uint32_t(((uint64_t(d[t + 1]) << 32) | d[t]) >> (8 * sh)));
     } else {
-#pragma unroll
-      for (int t = 0; t < 16; t++) W[t] = msg_word32(m, mlen, 64 * b + 4 * t);
+      msg_words32_tail(W, m, mlen, 64 * b);
     }
     if (b == nb - 1) {
       W[14] = uint32_t(mlen >> 29);

@@ -181,7 +181,11 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
     hd[k] = uint32_t(opaque_i32(int32_t(hd[k])));
     sd[k] = uint32_t(opaque_i32(int32_t(sd[k])));
   }
+#ifdef EDV_AB_UNIFORM_ATAB  // measurement-only variant (wrong verdicts): every lane reads slot 0's table
+  const GlobalATab at{a.st.atab};
+#else
   const GlobalATab at{a.st.atab + j * kAWords};
+#endif
   const GlobalBTab bt{a.btab};
   a.accept[i] = main_one(R, hd, sd, at, bt) ? 1 : 0;
 }
@@ -739,22 +743,37 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
     const uint8_t *src_s = sigs + 64 * a, *src_p = pks + 32 * a, *src_m = msgs + mA;
     const uint64_t* src_o = off + a;
     if (!pinned) {
+      // pageable: staged through this stream's pinned slot in up to four parts,
+      // each part's H2D queued as soon as it is staged, so the DMA of part j
+      // overlaps the parallel memcpy of part j + 1
       PinnedBuf& sl = c.stage[q];
       HIPOK(hipEventSynchronize(c.hs_staged[q]), "stage wait");  // the slot's previous H2D is done
       if (sl.ensure(cnt * 96 + (cnt + 1) * 8 + (mB - mA))) return EDV_E_OOM;
       uint8_t* p = static_cast<uint8_t*>(sl.p);
-      par_copy({{p, src_s, cnt * 64}, {p + cnt * 64, src_p, cnt * 32},
-                {p + cnt * 96, reinterpret_cast<const uint8_t*>(src_o), (cnt + 1) * 8},
-                {p + cnt * 96 + (cnt + 1) * 8, src_m, mB - mA}});
-      src_s = p;
-      src_p = p + cnt * 64;
-      src_o = reinterpret_cast<const uint64_t*>(p + cnt * 96);
-      src_m = p + cnt * 96 + (cnt + 1) * 8;
+      uint8_t *ps = p, *pp = p + cnt * 64, *po = p + cnt * 96, *pm = p + cnt * 96 + (cnt + 1) * 8;
+      const uint64_t bytes = cnt * 104 + (mB - mA);
+      const uint64_t parts = bytes >= (uint64_t(8) << 20) && cnt >= 4 ? 4 : 1;
+      for (uint64_t j = 0; j < parts; j++) {
+        const uint64_t r0 = cnt * j / parts, r1 = cnt * (j + 1) / parts;  // requests [a + r0, a + r1)
+        const uint64_t m0 = off[a + r0] - mA, m1 = off[a + r1] - mA;
+        par_copy({{ps + 64 * r0, src_s + 64 * r0, 64 * (r1 - r0)}, {pp + 32 * r0, src_p + 32 * r0, 32 * (r1 - r0)},
+                  {po + 8 * r0, reinterpret_cast<const uint8_t*>(src_o + r0), 8 * (r1 - r0 + 1)},
+                  {pm + m0, src_m + m0, m1 - m0}});
+        HIPOK(hipMemcpyAsync(d_sigs + 64 * (a - lo + r0), ps + 64 * r0, 64 * (r1 - r0), hipMemcpyHostToDevice, s),
+              "h2d sigs");
+        HIPOK(hipMemcpyAsync(d_pks + 32 * (a - lo + r0), pp + 32 * r0, 32 * (r1 - r0), hipMemcpyHostToDevice, s),
+              "h2d pks");
+        HIPOK(hipMemcpyAsync(d_o + r0, po + 8 * r0, 8 * (r1 - r0 + 1), hipMemcpyHostToDevice, s), "h2d off");
+        if (m1 > m0)
+          HIPOK(hipMemcpyAsync(d_msgs + (mA - mbase) + m0, pm + m0, m1 - m0, hipMemcpyHostToDevice, s), "h2d msgs");
+      }
+    } else {
+      HIPOK(hipMemcpyAsync(d_sigs + 64 * (a - lo), src_s, cnt * 64, hipMemcpyHostToDevice, s), "h2d sigs");
+      HIPOK(hipMemcpyAsync(d_pks + 32 * (a - lo), src_p, cnt * 32, hipMemcpyHostToDevice, s), "h2d pks");
+      HIPOK(hipMemcpyAsync(d_o, src_o, (cnt + 1) * 8, hipMemcpyHostToDevice, s), "h2d off");
+      if (mB > mA)
+        HIPOK(hipMemcpyAsync(d_msgs + (mA - mbase), src_m, mB - mA, hipMemcpyHostToDevice, s), "h2d msgs");
     }
-    HIPOK(hipMemcpyAsync(d_sigs + 64 * (a - lo), src_s, cnt * 64, hipMemcpyHostToDevice, s), "h2d sigs");
-    HIPOK(hipMemcpyAsync(d_pks + 32 * (a - lo), src_p, cnt * 32, hipMemcpyHostToDevice, s), "h2d pks");
-    HIPOK(hipMemcpyAsync(d_o, src_o, (cnt + 1) * 8, hipMemcpyHostToDevice, s), "h2d off");
-    if (mB > mA) HIPOK(hipMemcpyAsync(d_msgs + (mA - mbase), src_m, mB - mA, hipMemcpyHostToDevice, s), "h2d msgs");
     if (!pinned) HIPOK(hipEventRecord(c.hs_staged[q], s), "record");
     const bool bucket = bucketing_enabled(c, flags);
     VerifyArgs va = make_args(c, c.st, d_sigs + 64 * (a - lo), d_pks + 32 * (a - lo), d_msgs, d_o, mbase,
