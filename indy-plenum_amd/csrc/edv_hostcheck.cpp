@@ -96,12 +96,15 @@ void hc_sha256(const uint8_t* m, uint64_t mlen, int misalign, uint8_t* out32) {
 }
 void hc_btab(int32_t* out) { memcpy(out, btab().w.data(), sizeof(int32_t) * kBEntries * kBStride); }
 int hc_btab_entries() { return kBEntries; }
-// packed signed digits of a 32-byte scalar: radix 4 -> recode4 (h), 8 -> recode8 (signer), 16 -> recode16 (S)
+// packed signed digits of a 32-byte scalar: 5 -> recode5 (h, the main loop's windows),
+// 15 -> recode15 (S), 8 -> recode8 (signer), 4 / 16 -> the generic recoder at those radices
 int hc_recode(const uint8_t* in32, int bits, uint32_t* out8) {
   uint32_t w[8];
   load_words(w, in32, 8);
   if (bits == 4) recode4(out8, w);
+  else if (bits == 5) recode5(out8, w);
   else if (bits == 8) recode8(out8, w);
+  else if (bits == 15) recode15(out8, w);
   else if (bits == 16) recode16(out8, w);
   else return -1;
   return 0;

@@ -34,13 +34,13 @@ using namespace edv;
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kAWords = kAEntries * 40;   // cached point = 4 x 10 limbs (360 words = 1,440 B)
+constexpr int kAWords = kAEntries * 40;   // cached point = 4 x 10 limbs (680 words = 2,720 B)
 constexpr uint64_t kChunkDefault = uint64_t(1) << 18;  // signatures per prep/main launch pair
 
 // Per-chunk state handed from the prep kernel to the main kernel, SoA so every
 // wave-wide load/store touches 64 consecutive words:
-//   atab[360 * i + w]  word w (0..359) of signature i's 0..8 x (-A) table
-//   dig[w * cap + i]   w 0..7: packed radix-16 digits of h, 8..15: radix-2^16 digits of S
+//   atab[680 * i + w]  word w (0..679) of signature i's 0..16 x (-A) table
+//   dig[w * cap + i]   w 0..7: packed radix-32 digits of h, 8..15: radix-2^15 digits of S
 //   alive[i]           1 if V2-V5 passed (the main kernel skips dead lanes' work)
 struct ChunkState {
   int32_t* atab;
@@ -71,16 +71,16 @@ struct VerifyArgs {
 // 39 KB of L2-miss traffic per verify, 8x the useful bytes).
 struct GlobalATab {
   int32_t* slot;
-  __device__ __forceinline__ void store_fe(int word, const fe& f) const {
-    int2* p = reinterpret_cast<int2*>(slot + word);
-#pragma unroll
-    for (int q = 0; q < 5; q++) p[q] = make_int2(f.v[2 * q], f.v[2 * q + 1]);
-  }
+  // one entry = 40 contiguous words (160 B, 16-byte aligned): ten 16-byte stores
   __device__ __forceinline__ void store(int e, const ge_cached& c) const {
-    store_fe(e * 40 + 0, c.YpX);
-    store_fe(e * 40 + 10, c.YmX);
-    store_fe(e * 40 + 20, c.Z);
-    store_fe(e * 40 + 30, c.T2d);
+    int32_t t[40];
+#pragma unroll
+    for (int l = 0; l < 10; l++) {
+      t[l] = c.YpX.v[l]; t[10 + l] = c.YmX.v[l]; t[20 + l] = c.Z.v[l]; t[30 + l] = c.T2d.v[l];
+    }
+    int4* p = reinterpret_cast<int4*>(slot + e * 40);
+#pragma unroll
+    for (int q = 0; q < 10; q++) p[q] = make_int4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
   }
   __device__ __forceinline__ ge_cached load(int e) const {
     const int4* p = reinterpret_cast<const int4*>(slot + e * 40);
@@ -743,16 +743,18 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
     const uint8_t *src_s = sigs + 64 * a, *src_p = pks + 32 * a, *src_m = msgs + mA;
     const uint64_t* src_o = off + a;
     if (!pinned) {
-      // pageable: staged through this stream's pinned slot in up to four parts,
-      // each part's H2D queued as soon as it is staged, so the DMA of part j
-      // overlaps the parallel memcpy of part j + 1
+      // pageable: staged through this stream's pinned slot (a parallel memcpy),
+      // then copied by DMA.  Staging in four parts with each part's H2D queued as
+      // soon as it was staged measured slower at C2 (2.43 vs 1.78 ms per 64k:
+      // profiles/r02/e2e_probe_s6.json), the sixteen small copies costing more
+      // than the overlap saved.
       PinnedBuf& sl = c.stage[q];
       HIPOK(hipEventSynchronize(c.hs_staged[q]), "stage wait");  // the slot's previous H2D is done
       if (sl.ensure(cnt * 96 + (cnt + 1) * 8 + (mB - mA))) return EDV_E_OOM;
       uint8_t* p = static_cast<uint8_t*>(sl.p);
       uint8_t *ps = p, *pp = p + cnt * 64, *po = p + cnt * 96, *pm = p + cnt * 96 + (cnt + 1) * 8;
       const uint64_t bytes = cnt * 104 + (mB - mA);
-      const uint64_t parts = bytes >= (uint64_t(8) << 20) && cnt >= 4 ? 4 : 1;
+      const uint64_t parts = getenv("EDV_STAGE_PARTS") && bytes >= (uint64_t(8) << 20) && cnt >= 4 ? 4 : 1;
       for (uint64_t j = 0; j < parts; j++) {
         const uint64_t r0 = cnt * j / parts, r1 = cnt * (j + 1) / parts;  // requests [a + r0, a + r1)
         const uint64_t m0 = off[a + r0] - mA, m1 = off[a + r1] - mA;

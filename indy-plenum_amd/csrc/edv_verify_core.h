@@ -11,9 +11,21 @@
 
 namespace edv {
 
-constexpr int kAEntries = 9;   // per-lane table 0..8 x (-A), cached form (entry 0 = identity)
-constexpr int kBBits = 16;                     // radix 2^16 digits of S
-constexpr int kBEntries = (1 << (kBBits - 1)) + 1; // shared table 0..2^15 x B, affine precomp form (4 MiB)
+// [h](-A): 51 fixed signed windows of 5 bits (digits in [-16, 15], the top one in
+// [0, 8]) against a per-lane table 0..16 x (-A); [S]B: 17 signed radix-2^15
+// digits against a shared table 0..2^14 x B, one every third window (15 = 3 x 5
+// bits, so the B additions land on window boundaries).  Against 4-bit windows
+// (64 additions) and radix 2^16 (16 mixed additions): 13 fewer additions, one
+// more mixed addition, two fewer doublings per verify, and a 2 MiB B table that
+// fits one XCD's 4 MiB L2.
+constexpr int kAWin = 5;                        // bits per [h](-A) window
+constexpr int kAWindows = 51;                   // 51 x 5 = 255 bits >= 253
+constexpr int kAEntries = 17;                   // per-lane table 0..16 x (-A), cached form (entry 0 = identity)
+constexpr int kBBits = 15;                      // radix 2^15 digits of S
+constexpr int kBDigits = 17;                    // 17 x 15 = 255 bits >= 253
+constexpr int kBEvery = kBBits / kAWin;         // a B digit every third window
+constexpr int kBEntries = (1 << (kBBits - 1)) + 1; // shared table 0..2^14 x B, affine precomp form (2 MiB)
+static_assert(kBBits % kAWin == 0, "B digits must land on window boundaries");
 constexpr int kCombEntries = 129;               // signer comb rows: 0..128 x 256^i B
 constexpr int kBStride = 32;                    // words per B / comb entry (30 used; 128-byte aligned)
 
@@ -119,23 +131,33 @@ EDV_HD void hram(uint32_t out[16], const uint32_t R[8], const uint32_t A[8], con
 }
 
 // ------------------------------------------------------------ scalar recoding
-// h < L: 64 signed radix-16 digits in [-8, 7], packed 4-bit two's complement,
-// digit k at bits 4*(k%8) of word k/8.
-EDV_HD void recode4(uint32_t out[8], const uint32_t h[8]) {
+// NDIG signed radix-2^BITS digits of a 256-bit scalar s (8 little-endian words),
+// digit k in [-2^(BITS-1), 2^(BITS-1)) packed as BITS-bit two's complement at
+// bits [BITS k, BITS k + BITS) of out; the top digit takes the final carry and
+// stays non-negative (callers keep s < 2^253, so it stays in range).
+template <int BITS, int NDIG>
+EDV_HD void recode_signed(uint32_t out[8], const uint32_t s[8]) {
+  static_assert(BITS * NDIG <= 256 && BITS <= 31, "digits must fit 256 bits");
+  constexpr uint32_t kMask = (1u << BITS) - 1;
+#pragma unroll
+  for (int w = 0; w < 8; w++) out[w] = 0;
   int carry = 0;
 #pragma unroll
-  for (int w = 0; w < 8; w++) {
-    uint32_t packed = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      int e = int((h[w] >> (4 * k)) & 15) + carry;
-      carry = (w == 7 && k == 7) ? 0 : ((e + 8) >> 4);
-      e -= carry * 16;
-      packed |= uint32_t(e & 15) << (4 * k);
-    }
-    out[w] = packed;
+  for (int k = 0; k < NDIG; k++) {
+    const int pos = BITS * k, wi = pos >> 5, sh = pos & 31;
+    const uint64_t win = uint64_t(s[wi]) | (wi + 1 < 8 ? uint64_t(s[wi + 1]) << 32 : 0);
+    int e = int(uint32_t(win >> sh) & kMask) + carry;
+    carry = (k == NDIG - 1) ? 0 : ((e + (1 << (BITS - 1))) >> BITS);
+    e -= carry * (1 << BITS);
+    const uint64_t pe = uint64_t(uint32_t(e) & kMask) << sh;
+    out[wi] |= uint32_t(pe);
+    if (wi + 1 < 8) out[wi + 1] |= uint32_t(pe >> 32);
   }
 }
+// h < L: the 51 radix-32 digits of the [h](-A) windows
+EDV_HD void recode5(uint32_t out[8], const uint32_t h[8]) { recode_signed<kAWin, kAWindows>(out, h); }
+// h < L: 64 signed radix-16 digits in [-8, 7] (kept for the recoding tests)
+EDV_HD void recode4(uint32_t out[8], const uint32_t h[8]) { recode_signed<4, 64>(out, h); }
 // S (signer scalars): 32 signed radix-256 digits in [-128, 127] (k < 2^253 keeps
 // the top digit <= 32).
 EDV_HD void recode8(uint32_t out[8], const uint32_t s[8]) {
@@ -153,24 +175,10 @@ EDV_HD void recode8(uint32_t out[8], const uint32_t s[8]) {
     out[w] = packed;
   }
 }
-// S (verify, V8): 16 signed radix-2^16 digits in [-2^15, 2^15), packed as 16-bit
-// two's complement, digit k at bits 16*(k%2) of word k/2.  V2 leaves S < 2^253,
-// so the top digit is <= 2^13 + 1 and stays inside the 0..2^15 table.
-EDV_HD void recode16(uint32_t out[8], const uint32_t s[8]) {
-  int carry = 0;
-#pragma unroll
-  for (int w = 0; w < 8; w++) {
-    uint32_t packed = 0;
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      int e = int((s[w] >> (16 * k)) & 0xffff) + carry;
-      carry = (w == 7 && k == 1) ? 0 : ((e + 0x8000) >> 16);
-      e -= carry * 0x10000;
-      packed |= uint32_t(e & 0xffff) << (16 * k);
-    }
-    out[w] = packed;
-  }
-}
+// S (verify, V8): 17 signed radix-2^15 digits in [-2^14, 2^14).  V2 leaves
+// S < 2^253, so the top digit is <= 2^13 and stays inside the 0..2^14 table.
+EDV_HD void recode15(uint32_t out[8], const uint32_t s[8]) { recode_signed<kBBits, kBDigits>(out, s); }
+EDV_HD void recode16(uint32_t out[8], const uint32_t s[8]) { recode_signed<16, 16>(out, s); }
 // shift a 256-bit little-endian word vector left by N bits (0 < N < 32)
 template <int N>
 EDV_HD void shl256(uint32_t v[8]) {
@@ -210,7 +218,7 @@ EDV_HD void btab_entry(int32_t* o, int j) {
 
 // Phase 1 of one signature (kernel edv_prep_kernel): strictness checks V2-V4,
 // decompression V5, h = SHA-512(R || A || M) mod L (V6, V7), digit recoding and
-// the 0..8 x (-A) table (entry 0 the identity, so a zero digit needs no select).  Returns false if the signature is already rejected
+// the 0..16 x (-A) table (entry 0 the identity, so a zero digit needs no select).  Returns false if the signature is already rejected
 // (then hd/sd/table are unspecified).  ATab provides store(e, cached).
 template <class ATab>
 EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen,
@@ -224,8 +232,8 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
   uint32_t dig[16], h[8];
   hram(dig, R, A, m, mlen);
   sc_reduce(h, dig);
-  recode4(hd, h);
-  recode16(sd, S);
+  recode5(hd, h);
+  recode15(sd, S);
   const ge_cached c1 = ge_p3_to_cached(nA);
   at.store(0, ge_cached_identity());
   at.store(1, c1);
@@ -241,23 +249,26 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
 
 // Phase 2 (kernel edv_main_kernel): V8 R' = [h](-A) + [S]B by a joint
 // fixed-window walk, top digit first -- every lane adds at the same positions,
-// so a wave never diverges -- then V9 encode(R') == R.  [S]B adds one radix-2^16
-// digit every fourth window (16 mixed additions instead of 32 at radix 256).  ATab provides load(e);
-// BTab provides entry(j) -> precomp.
+// so a wave never diverges -- then V9 encode(R') == R.  51 windows of 5 bits for
+// [h](-A) (one table addition each); [S]B adds one radix-2^15 digit every third
+// window.  ATab provides load(e); BTab provides entry(j) -> precomp.
 template <class ATab, class BTab>
 EDV_HD bool main_one(const uint32_t R[8], uint32_t hd[8], uint32_t sd[8], const ATab& at, const BTab& bt) {
   ge_p2 acc = ge_p2_identity();
+  int bphase = (kAWindows - 1) % kBEvery;  // windows until the next B digit
 #pragma unroll 1
-  for (int w = 63; w >= 0; --w) {
+  for (int w = kAWindows - 1; w >= 0; --w) {
     // table reads first, so their latency hides under this window's doublings
-    const int dA = int32_t(hd[7]) >> 28;
-    shl256<4>(hd);
+    const int dA = int32_t(hd[7] << 1) >> (32 - kAWin);  // digit at bits [250, 255)
+    shl256<kAWin>(hd);
     ge_cached c = at.load(dA < 0 ? -dA : dA);
+    const bool addB = bphase == 0;
+    bphase = addB ? kBEvery - 1 : bphase - 1;
     int dB = 0;
     ge_precomp q;
-    if ((w & 3) == 0) {
-      dB = int32_t(sd[7]) >> 16;
-      shl256<16>(sd);
+    if (addB) {
+      dB = int32_t(sd[7] << 1) >> (32 - kBBits);  // digit at bits [240, 255)
+      shl256<kBBits>(sd);
       // shift before the loads are issued: scheduled after them, the shift's
       // temporaries landed in the loads' destination VGPRs and forced a vmcnt
       // wait right behind the loads
@@ -265,17 +276,16 @@ EDV_HD bool main_one(const uint32_t R[8], uint32_t hd[8], uint32_t sd[8], const 
       q = bt.entry(dB < 0 ? -dB : dB);
     }
     ge_p3 p3;
-    if (w == 63) {
+    if (w == kAWindows - 1) {
       p3 = ge_p3_identity();
     } else {
-      acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
-      acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
-      acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
+#pragma unroll
+      for (int d = 0; d < kAWin - 1; d++) acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
       p3 = ge_p1p1_to_p3(ge_p2_dbl(acc));
     }
     c = ge_cached_cneg(c, dA < 0);
     ge_p1p1 t = ge_add(p3, c);
-    if ((w & 3) == 0) {
+    if (addB) {
       p3 = ge_p1p1_to_p3(t);
       t = ge_madd(p3, ge_precomp_cneg(q, dB < 0));
     }

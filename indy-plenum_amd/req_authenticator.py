@@ -61,7 +61,39 @@ class ReqAuthenticator:
         with gc_paused():
             return self._authenticate_batch(reqs)
 
+    def _single_stock(self, reqs):
+        """Fast path for the usual node set-up, one authenticator whose batch path
+        is the stock read-only one: list-comprehension passes only, the type
+        predicates evaluated once per distinct type.  None = use the general path
+        (several authenticators, a malformed request, an unhashable type, a
+        predicate that raises)."""
+        if len(self._authenticators) != 1:
+            return None
+        a = self._authenticators[0]
+        ro = getattr(a, "batch_reads_only", None)
+        if not hasattr(a, "authenticate_batch") or ro is None or not ro():
+            return None
+        try:
+            typs = [req.get(OPERATION, {}).get(TXN_TYPE) for req in reqs]
+            kinds = {t: (0 if a.is_query(t) else (2 if a.is_write(t) or a.is_action(t) else 1)) for t in set(typs)}
+        except Exception:
+            return None
+        kd = [kinds[t] for t in typs]
+        todo = [k for k, x in enumerate(kd) if x == 2]
+        out = [set() if x == 0 else None for x in kd]
+        results = a.authenticate_batch([reqs[k] for k in todo])
+        for k, rv in zip(todo, results):
+            # authenticate(): identifiers.update(rv or set()); none -> NoAuthenticatorFound
+            out[k] = rv if isinstance(rv, BaseException) else (set(rv) if rv else NoAuthenticatorFound())
+        for k, x in enumerate(kd):
+            if x == 1:
+                out[k] = NoAuthenticatorFound()
+        return out
+
     def _authenticate_batch(self, reqs):
+        fast = self._single_stock(reqs)
+        if fast is not None:
+            return fast
         n = len(reqs)
         out = [None] * n
         typs = [None] * n

@@ -152,18 +152,20 @@ def test_kernel_algorithm_on_cpu_matches_libsodium_golden(golden, golden_meta):
 
 
 def _digits(packed, bits):
-    per = 32 // bits
+    """Digit k at bits [bits k, bits k + bits) of the packed 256-bit value."""
+    v = sum(w << (32 * i) for i, w in enumerate(packed))
     out = []
     for k in range(256 // bits):
-        raw = (packed[k // per] >> (bits * (k % per))) & ((1 << bits) - 1)
+        raw = (v >> (bits * k)) & ((1 << bits) - 1)
         out.append(raw - (1 << bits) if raw >> (bits - 1) else raw)
     return out
 
 
-def test_scalar_recoding_radix_4_8_16():
-    """Signed digits the main loop consumes: h (radix 16, digit in [-8, 7]),
-    S (radix 2^16, |d| <= 2^15 so it indexes the 0..2^15 B table) and signer
-    scalars (radix 256); sum d_k * 2^(bits*k) must give back the scalar."""
+def test_scalar_recoding_radix_4_5_8_15_16():
+    """Signed digits the main loop consumes: h (radix 32, digit in [-16, 15], so
+    |d| indexes the 0..16 per-lane table), S (radix 2^15, |d| <= 2^14 so it
+    indexes the 0..2^14 B table), signer scalars (radix 256), and the generic
+    recoder at radix 16 / 2^16; sum d_k * 2^(bits*k) must give back the scalar."""
     hc = hostcheck_lib.load()
     r = random.Random(12)
     out = (ctypes.c_uint32 * 8)()
@@ -172,7 +174,7 @@ def test_scalar_recoding_radix_4_8_16():
     edge += [int("8000" * 16, 16) % L, int("7fff" * 16, 16) % L, int("ffff" * 15, 16), int("80" * 31, 16)]
     edge += [int("88" * 31, 16), int("77" * 31, 16)]
     vals = [v for v in edge if 0 <= v < L] + [r.randrange(L) for _ in range(2000)]
-    for bits, lo, hi in ((4, -8, 7), (8, -128, 127), (16, -2**15, 2**15)):
+    for bits, lo, hi in ((4, -8, 7), (5, -16, 15), (8, -128, 127), (15, -2**14, 2**14), (16, -2**15, 2**15)):
         for v in vals:
             assert hc.hc_recode(v.to_bytes(32, "little"), bits, out) == 0
             d = _digits(list(out), bits)
@@ -182,16 +184,16 @@ def test_scalar_recoding_radix_4_8_16():
 
 
 def test_btab_entries_are_multiples_of_B():
-    """The 0..2^15 x B table (affine y+x, y-x, 2dxy limbs) against the oracle's [j]B."""
+    """The 0..2^14 x B table (affine y+x, y-x, 2dxy limbs) against the oracle's [j]B."""
     import oracle_lib as orc
     hc = hostcheck_lib.load()
     n = hc.hc_btab_entries()
-    assert n == 2**15 + 1
+    assert n == 2**14 + 1
     tab = (ctypes.c_int32 * (n * 32))()
     hc.hc_btab(tab)
     d = (-121665 * pow(121666, P - 2, P)) % P
     r = random.Random(13)
-    for j in [0, 1, 2, 3, 127, 128, 129, 255, 256, 4097, 32767, 32768] + [r.randrange(n) for _ in range(40)]:
+    for j in [0, 1, 2, 3, 127, 128, 129, 255, 256, 4097, 16383, 16384] + [r.randrange(n) for _ in range(40)]:
         e = list(tab[32 * j: 32 * j + 32])
         ypx, ymx, xy2d = val(e[0:10]) % P, val(e[10:20]) % P, val(e[20:30]) % P
         inv2 = pow(2, P - 2, P)
