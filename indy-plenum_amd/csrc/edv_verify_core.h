@@ -235,13 +235,17 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
   recode5(hd, h);
   recode15(sd, S);
   const ge_cached c1 = ge_p3_to_cached(nA);
+  // -A comes out of the decompression affine (Z = 1, T = XY), so its cached form
+  // doubles as precomp form and each further entry is a mixed addition (3 field
+  // products instead of 4: 14 products saved per signature)
+  const ge_precomp p1{c1.YpX, c1.YmX, c1.T2d};
   at.store(0, ge_cached_identity());
   at.store(1, c1);
   ge_p3 cur = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(nA)));
   at.store(2, ge_p3_to_cached(cur));
 #pragma unroll 1
   for (int e = 3; e < kAEntries; e++) {
-    cur = ge_p1p1_to_p3(ge_add(cur, c1));
+    cur = ge_p1p1_to_p3(ge_madd(cur, p1));
     at.store(e, ge_p3_to_cached(cur));
   }
   return true;

@@ -36,7 +36,11 @@ def nym_messages(n, seed=0x5EED2025, start=0, msg_len=256, var_range=None):
     off[1:] = np.cumsum(lens)
     fields = rng.integers(0, 256, size=(n, 48), dtype=np.uint8)
     idh, dh, vh = _hex_cols(fields[:, :16]), _hex_cols(fields[:, 16:32]), _hex_cols(fields[:, 32:])
-    req = np.array([b"%016d" % (1539648000000000 + start + i) for i in range(n)]).view(np.uint8).reshape(n, 16)
+    # reqId = 1539648000000000 + global index, 16 decimal digits (vectorised: C3 builds 16M)
+    rid = np.uint64(1539648000000000 + start) + np.arange(n, dtype=np.uint64)
+    req = np.empty((n, 16), dtype=np.uint8)
+    for d in range(16):
+        req[:, 15 - d] = (rid // np.uint64(10 ** d) % np.uint64(10)).astype(np.uint8) + ord('0')
 
     def lit(s):
         return np.broadcast_to(np.frombuffer(s, dtype=np.uint8), (n, len(s)))
@@ -99,21 +103,30 @@ class DeviceBatch:
             self._damage()
 
     def _damage(self):
+        """Vectorised over the damaged positions (C3 damages 800k of 16M)."""
         L = 2**252 + 27742317777372353535851937790883648493
         sigs = self.d_sigs.download(64 * self.n).copy()
         pks = self.d_pks.download(32 * self.n).copy()
         msgs = self.host_msgs.copy()
-        for k, i in enumerate(self.bad.tolist()):
-            kind = (self.start + i) % 4
-            if kind == 0:
-                sigs[64 * i + 5] ^= 0x10                                    # R bit
-            elif kind == 1:
-                s = int.from_bytes(sigs[64 * i + 32:64 * i + 64].tobytes(), "little") + L
-                sigs[64 * i + 32:64 * i + 64] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)  # S + L
-            elif kind == 2:
-                msgs[int(self.host_off[i]) + 3] ^= 0x01                     # message byte
-            else:
-                pks[32 * i + 9] ^= 0x04                                     # key bit
+        bad = self.bad
+        kind = (self.start + bad) % 4
+        i0, i1, i2, i3 = (bad[kind == k] for k in range(4))
+        sigs[64 * i0 + 5] ^= 0x10                                           # R bit
+        if i1.size:                                                         # S + L (256-bit add)
+            sv = sigs.reshape(self.n, 64)[i1, 32:].copy().view(np.uint64)   # 4 little-endian limbs
+            lw = [np.uint64((L >> (64 * k)) & (2**64 - 1)) for k in range(4)]
+            carry = np.zeros(len(i1), dtype=np.uint64)
+            for k in range(4):
+                a = sv[:, k]
+                t = a + lw[k]
+                c1 = (t < a).astype(np.uint64)
+                t2 = t + carry
+                c2 = (t2 < t).astype(np.uint64)
+                sv[:, k] = t2
+                carry = c1 | c2
+            sigs.reshape(self.n, 64)[i1, 32:] = sv.view(np.uint8).reshape(len(i1), 32)
+        msgs[self.host_off[i2].astype(np.int64) + 3] ^= 0x01                # message byte
+        pks[32 * i3 + 9] ^= 0x04                                            # key bit
         self.d_sigs.upload(sigs)
         self.d_pks.upload(pks)
         self.host_msgs = msgs
