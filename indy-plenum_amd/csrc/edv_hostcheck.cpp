@@ -19,10 +19,13 @@ struct HostATab {
 };
 struct HostBTab {
   std::vector<int32_t> w;
-  HostBTab() : w(kBEntries * kBStride) {
-    for (int j = 0; j < kBEntries; j++) btab_entry(w.data() + j * kBStride, j);
+  HostBTab() : w(kBTables * kBEntries * kBStride) {
+    for (int t = 0; t < kBTables; t++) {
+      const ge_p3 base = base_point(t * kBSplit);
+      for (int j = 0; j < kBEntries; j++) btab_entry(w.data() + (t * kBEntries + j) * kBStride, j, base);
+    }
   }
-  ge_precomp entry(int j) const { return precomp_from_words(w.data() + j * kBStride); }
+  ge_precomp entry(int t, int j) const { return precomp_from_words(w.data() + (t * kBEntries + j) * kBStride); }
 };
 struct HostComb {
   std::vector<int32_t> w;
@@ -95,6 +98,28 @@ void hc_sha256(const uint8_t* m, uint64_t mlen, int misalign, uint8_t* out32) {
   store_words(out32, o, 8);
 }
 void hc_btab(int32_t* out) { memcpy(out, btab().w.data(), sizeof(int32_t) * kBEntries * kBStride); }
+// table t (0: j B, 1: j 2^130 B)
+int hc_btab_table(int t, int32_t* out) {
+  if (t < 0 || t >= kBTables) return -1;
+  memcpy(out, btab().w.data() + size_t(t) * kBEntries * kBStride, sizeof(int32_t) * kBEntries * kBStride);
+  return 0;
+}
+// the lattice reduction of the prep kernel: (a, u, neg) for h (32-byte scalars)
+int hc_half_scalars(const uint8_t* h32, uint8_t* a32, uint8_t* u32) {
+  uint32_t h[8], a[8], u[8];
+  load_words(h, h32, 8);
+  bool neg = false;
+  half_scalars(h, a, u, neg);
+  store_words(a32, a, 8);
+  store_words(u32, u, 8);
+  return neg ? 1 : 0;
+}
+// B-scalar digit pairs of s (9 words)
+void hc_recode_bscalar(const uint8_t* s32, uint32_t* out9) {
+  uint32_t s[8];
+  load_words(s, s32, 8);
+  recode_bscalar(out9, s);
+}
 int hc_btab_entries() { return kBEntries; }
 // packed signed digits of a 32-byte scalar: 5 -> recode5 (h, the main loop's windows),
 // 15 -> recode15 (S), 8 -> recode8 (signer), 4 / 16 -> the generic recoder at those radices
@@ -135,8 +160,8 @@ int hc_verify_batch(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs
     const uint64_t mlen = off[i + 1] - off[i];
     std::vector<uint8_t> buf(mlen + 32, 0);
     if (mlen) memcpy(buf.data() + 16, msgs + off[i], mlen);
-    HostATab at;
-    accept[i] = verify_one(R, S, A, buf.data() + 16, mlen, at, bt) ? 1 : 0;
+    HostATab at, rt;
+    accept[i] = verify_one(R, S, A, buf.data() + 16, mlen, at, rt, bt) ? 1 : 0;
   }
   return 0;
 }

@@ -35,15 +35,22 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kAWords = kAEntries * 40;   // cached point = 4 x 10 limbs (680 words = 2,720 B)
+// dig words per signature: da (8), db (8), B digit pairs (9), window count (1)
+constexpr int kDigWords = 8 + 8 + kBDigits + 1;
+constexpr int kDigB = 16, kDigNwin = 16 + kBDigits;
 constexpr uint64_t kChunkDefault = uint64_t(1) << 18;  // signatures per prep/main launch pair
 
 // Per-chunk state handed from the prep kernel to the main kernel, SoA so every
 // wave-wide load/store touches 64 consecutive words:
 //   atab[680 * i + w]  word w (0..679) of signature i's 0..16 x (-A) table
-//   dig[w * cap + i]   w 0..7: packed radix-32 digits of h, 8..15: radix-2^15 digits of S
-//   alive[i]           1 if V2-V5 passed (the main kernel skips dead lanes' work)
+//   rtab[680 * i + w]  the same for its 0..16 x (-+R) table
+//   dig[w * cap + i]   w 0..7: packed radix-32 digits of a, 8..15: of |b|,
+//                      16..24: B-scalar digit pairs, 25: windows needed
+//   alive[i]           1 if the A-side prep checks passed; alive[cap + i]: the R side
+//                      (the main kernel skips lanes where either is 0)
 struct ChunkState {
   int32_t* atab;
+  int32_t* rtab;
   uint32_t* dig;
   uint8_t* alive;
   uint64_t cap;
@@ -60,7 +67,7 @@ struct VerifyArgs {
   uint64_t n;             // signatures in this chunk
   uint8_t* accept;        // indexed by global signature index
   ChunkState st;
-  const int32_t* btab;    // kBEntries x kBStride
+  const int32_t* btab;    // kBTables x kBEntries x kBStride
 };
 
 // ---------------------------------------------------------------- kernels
@@ -98,13 +105,13 @@ struct GlobalATab {
     return c;
   }
 };
-// Shared 0..2^15 x B table in global memory (4 MiB, L2/MALL-resident), read as
-// 16-byte vectors: too large for LDS, and each lane touches one 128-byte entry
-// every fourth window.
+// Shared 0..2^14 x B and 0..2^14 x 2^130 B tables in global memory (2 x 2 MiB,
+// L2/MALL-resident), read as 16-byte vectors: too large for LDS, and each lane
+// touches one 128-byte entry of each every third window.
 struct GlobalBTab {
   const int32_t* w;
-  __device__ __forceinline__ ge_precomp entry(int j) const {
-    const int4* p = reinterpret_cast<const int4*>(w + j * kBStride);
+  __device__ __forceinline__ ge_precomp entry(int tb, int j) const {
+    const int4* p = reinterpret_cast<const int4*>(w + (tb * kBEntries + j) * kBStride);
     int32_t t[32];
 #pragma unroll
     for (int i = 0; i < 7; i++) {
@@ -115,7 +122,7 @@ struct GlobalBTab {
     // allocator reuse their VGPRs as temporaries, which forced a vmcnt wait
     // on the whole entry before the window's doublings (the opaque offset
     // keeps LLVM from widening this 8-byte load back to 16 bytes)
-    const int2 v = *reinterpret_cast<const int2*>(w + j * kBStride + opaque_i32(28));
+    const int2 v = *reinterpret_cast<const int2*>(w + (tb * kBEntries + j) * kBStride + opaque_i32(28));
     t[28] = v.x; t[29] = v.y;
     return precomp_from_words(t);
   }
@@ -130,13 +137,30 @@ __device__ __forceinline__ void load_words(uint32_t* out, const uint32_t* p, int
   }
 }
 
-// Phase 1: V2-V7, digit recoding, the per-signature A table.
+// Phase 1: V2-V7, half-size scalars, digit recoding and the A table (even
+// workgroups), R decompression and the R table (odd workgroups).  The two
+// halves share no data, so they run side by side: two waves per SIMD at 64k
+// signatures instead of one, each hiding the other's latencies.
+__device__ __forceinline__ void prep_r_side(const VerifyArgs& a, uint64_t j) {
+  if (j >= a.n) return;
+  const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
+  uint32_t R[8];
+  load_words(R, a.sigs + 16 * i, 2);
+  GlobalATab rt{a.st.rtab + j * kAWords};
+  const bool ok = prep_r(R, rt);
+  a.st.alive[a.st.cap + j] = ok ? 1 : 0;
+  if (!ok) a.accept[i] = 0;
+}
 #ifndef EDV_PREP_WAVES
 #define EDV_PREP_WAVES 2  // minimum waves per SIMD the prep kernel's register budget must allow
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EDV_PREP_WAVES, 8))) void edv_prep_kernel(
     VerifyArgs a) {
-  const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;  // slot within the chunk
+  const uint64_t j = uint64_t(blockIdx.x >> 1) * kBlock + threadIdx.x;  // slot within the chunk
+  if (blockIdx.x & 1) {
+    prep_r_side(a, j);
+    return;
+  }
   if (j >= a.n) return;
   const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
   uint32_t R[8], S[8], A[8];
@@ -145,32 +169,47 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EDV_PREP
   load_words(A, a.pks + 8 * i, 2);
   const uint64_t o0 = a.off[i] - a.msg_base, o1 = a.off[i + 1] - a.msg_base;
   GlobalATab at{a.st.atab + j * kAWords};
-  uint32_t hd[8], sd[8];
-  const bool ok = prep_one(R, S, A, a.msgs + o0, o1 - o0, at, hd, sd);
+  PrepDigits pd;
+  const bool ok = prep_one(R, S, A, a.msgs + o0, o1 - o0, at, pd);
   a.st.alive[j] = ok ? 1 : 0;
   if (ok) {
+    uint32_t* d = a.st.dig + j;
+    const uint64_t cap = a.st.cap;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      a.st.dig[uint64_t(k) * a.st.cap + j] = hd[k];
-      a.st.dig[uint64_t(8 + k) * a.st.cap + j] = sd[k];
+      d[uint64_t(k) * cap] = pd.da[k];
+      d[uint64_t(8 + k) * cap] = pd.db[k];
     }
+#pragma unroll
+    for (int k = 0; k < kBDigits; k++) d[uint64_t(kDigB + k) * cap] = pd.bw[k];
+    d[uint64_t(kDigNwin) * cap] = uint32_t(pd.nwin) | (pd.negR ? 0x100u : 0u);
   } else {
     a.accept[i] = 0;
   }
 }
 
-// Phase 2: V8 double-scalar multiplication and V9 compare (~85% of the work).
+// Phase 2: V8 multi-scalar walk and the identity check.  The window count is
+// the wave's maximum over its live lanes, so the loop stays wave-uniform.
 __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= a.n || !a.st.alive[j]) return;
+  const bool live = j < a.n && a.st.alive[j] && a.st.alive[a.st.cap + j];
+  const uint32_t* d = a.st.dig + j;
+  const uint64_t cap = a.st.cap;
+  const uint32_t wf = live ? d[uint64_t(kDigNwin) * cap] : 0;
+  int nwin = int(wf & 0xff);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nwin = max(nwin, __shfl_xor(nwin, o));
+  nwin = __builtin_amdgcn_readfirstlane(nwin);
+  if (!live) return;
   const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
-  uint32_t R[8], hd[8], sd[8];
-  load_words(R, a.sigs + 16 * i, 2);
+  uint32_t da[8], db[8], bw[kBDigits];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    hd[k] = a.st.dig[uint64_t(k) * a.st.cap + j];
-    sd[k] = a.st.dig[uint64_t(8 + k) * a.st.cap + j];
+    da[k] = d[uint64_t(k) * cap];
+    db[k] = d[uint64_t(8 + k) * cap];
   }
+#pragma unroll
+  for (int k = 0; k < kBDigits; k++) bw[k] = d[uint64_t(kDigB + k) * cap];
   // Settle the digit loads here, once: the digit registers are shifted inside
   // the window loop, and the waitcnt pass, merging the loop's back edge with
   // loads still pending from the preheader, otherwise inserts vmcnt waits at
@@ -178,16 +217,14 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   // stalled on its table reads; 9.5 % of wave cycles in SQ_WAIT_ANY).
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    hd[k] = uint32_t(opaque_i32(int32_t(hd[k])));
-    sd[k] = uint32_t(opaque_i32(int32_t(sd[k])));
+    da[k] = uint32_t(opaque_i32(int32_t(da[k])));
+    db[k] = uint32_t(opaque_i32(int32_t(db[k])));
   }
-#ifdef EDV_AB_UNIFORM_ATAB  // measurement-only variant (wrong verdicts): every lane reads slot 0's table
-  const GlobalATab at{a.st.atab};
-#else
-  const GlobalATab at{a.st.atab + j * kAWords};
-#endif
+#pragma unroll
+  for (int k = 0; k < kBDigits; k++) bw[k] = uint32_t(opaque_i32(int32_t(bw[k])));
+  const GlobalATab at{a.st.atab + j * kAWords}, rt{a.st.rtab + j * kAWords};
   const GlobalBTab bt{a.btab};
-  a.accept[i] = main_one(R, hd, sd, at, bt) ? 1 : 0;
+  a.accept[i] = main_one(da, db, bw, nwin, (wf >> 8) & 1, at, rt, bt) ? 1 : 0;
 }
 
 // Comb rows for the batch signer, in global memory (528 KB, L2-resident).
@@ -284,10 +321,10 @@ __global__ __launch_bounds__(kBlock) void edv_bucket_scatter_kernel(const uint64
   if (j < n) perm[wbase[b] + rank] = uint32_t(j);
 }
 
-// j * B for j = 0..2^15 in affine precomp form, once per device
+// j * B and j * 2^130 B for j = 0..2^14 in affine precomp form, once per device
 __global__ void edv_btab_kernel(int32_t* out) {
-  const int j = threadIdx.x + blockIdx.x * blockDim.x;
-  if (j < kBEntries) btab_entry(out + j * kBStride, j);
+  const int t = threadIdx.x + blockIdx.x * blockDim.x;
+  if (t < kBTables * kBEntries) btab_entry(out + t * kBStride, t % kBEntries, base_point((t / kBEntries) * kBSplit));
 }
 
 // Row f-3: SHA-256 of n messages, one per lane -> 32-byte digests (out: n x 8 words).
@@ -372,10 +409,11 @@ constexpr int kQ = 4;
 
 // One set of per-chunk state buffers (ChunkState storage + bucket permutation).
 struct ChunkBufs {
-  DevBuf atab, dig, alive;  // ChunkState storage for `chunk` signatures (~400 MB at 2^18)
+  DevBuf atab, rtab, dig, alive;  // ChunkState storage for `chunk` signatures (~1.4 GB at 2^18)
   DevBuf perm, bucket_ctr;  // length-bucket permutation of a chunk; histogram + cursors (one set per stream)
   int ensure(uint64_t chunk) {
-    if (atab.ensure(chunk * kAWords * 4) || dig.ensure(chunk * 16 * 4) || alive.ensure(chunk) ||
+    if (atab.ensure(chunk * kAWords * 4) || rtab.ensure(chunk * kAWords * 4) || dig.ensure(chunk * kDigWords * 4) ||
+        alive.ensure(2 * chunk) ||
         perm.ensure(chunk * 4) || bucket_ctr.ensure(uint64_t(kQ) * 2 * kBuckets * 4))
       return EDV_E_OOM;
     return 0;
@@ -464,9 +502,9 @@ int ctx_init(DevCtx& c) {
     if (v >= kBlock && v <= (uint64_t(1) << 24)) c.chunk = (v / kBlock) * kBlock;
   }
   if (c.st.ensure(c.chunk)) return EDV_E_OOM;
-  if (!c.btab) HIPOK(hipMalloc(&c.btab, kBEntries * kBStride * 4), "hipMalloc btab");
+  if (!c.btab) HIPOK(hipMalloc(&c.btab, kBTables * kBEntries * kBStride * 4), "hipMalloc btab");
   if (!c.btab_built) {
-    edv_btab_kernel<<<(kBEntries + 63) / 64, 64, 0, c.stream>>>(c.btab);
+    edv_btab_kernel<<<(kBTables * kBEntries + 63) / 64, 64, 0, c.stream>>>(c.btab);
     HIPOK(hipGetLastError(), "btab launch");
     HIPOK(hipStreamSynchronize(c.stream), "btab sync");
     c.btab_built = true;
@@ -516,7 +554,8 @@ VerifyArgs make_args(const DevCtx& c, ChunkBufs& b, const uint8_t* d_sigs, const
   va.msg_base = msg_base;
   va.accept = d_accept;
   // slots [slot0, slot0 + n) of the chunk scratch (dig stays indexed w * cap + slot)
-  va.st = ChunkState{static_cast<int32_t*>(b.atab.p) + slot0 * kAWords, static_cast<uint32_t*>(b.dig.p) + slot0,
+  va.st = ChunkState{static_cast<int32_t*>(b.atab.p) + slot0 * kAWords, static_cast<int32_t*>(b.rtab.p) + slot0 * kAWords,
+                     static_cast<uint32_t*>(b.dig.p) + slot0,
                      static_cast<uint8_t*>(b.alive.p) + slot0, c.chunk,
                      bucket ? static_cast<uint32_t*>(b.perm.p) + slot0 : nullptr};
   va.btab = c.btab;
@@ -535,7 +574,7 @@ int launch_prep(uint32_t* ctr, const VerifyArgs& va, const uint64_t* d_off, bool
                                                                      const_cast<uint32_t*>(va.st.perm));
     HIPOK(hipGetLastError(), "bucket launch");
   }
-  edv_prep_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
+  edv_prep_kernel<<<dim3(2 * blocks), dim3(kBlock), 0, s>>>(va);  // A and R sides
   HIPOK(hipGetLastError(), "prep launch");
   return 0;
 }
@@ -1138,7 +1177,7 @@ int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uin
                                                                                const_cast<uint32_t*>(va.st.perm));
     }
     HIPOK(hipEventRecord(ev.e[0], c->stream), "record");
-    edv_prep_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(va);
+    edv_prep_kernel<<<dim3(2 * blocks), dim3(kBlock), 0, c->stream>>>(va);
     HIPOK(hipEventRecord(ev.e[1], c->stream), "record");
     edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(va);
     HIPOK(hipEventRecord(ev.e[2], c->stream), "record");

@@ -11,20 +11,35 @@
 
 namespace edv {
 
-// [h](-A): 51 fixed signed windows of 5 bits (digits in [-16, 15], the top one in
-// [0, 8]) against a per-lane table 0..16 x (-A); [S]B: 17 signed radix-2^15
-// digits against a shared table 0..2^14 x B, one every third window (15 = 3 x 5
-// bits, so the B additions land on window boundaries).  Against 4-bit windows
-// (64 additions) and radix 2^16 (16 mixed additions): 13 fewer additions, one
-// more mixed addition, two fewer doublings per verify, and a 2 MiB B table that
-// fits one XCD's 4 MiB L2.
-constexpr int kAWin = 5;                        // bits per [h](-A) window
-constexpr int kAWindows = 51;                   // 51 x 5 = 255 bits >= 253
-constexpr int kAEntries = 17;                   // per-lane table 0..16 x (-A), cached form (entry 0 = identity)
-constexpr int kBBits = 15;                      // radix 2^15 digits of S
-constexpr int kBDigits = 17;                    // 17 x 15 = 255 bits >= 253
+// Half-size scalars (V8).  libsodium's R' = [S]B + [h](-A)
+// with a 253-bit h costs 252 doublings.  Instead the prep kernel finds, by a
+// 2-dimensional lattice reduction, a ~128-bit pair (a, b) with a = b h (mod 8L)
+// and b odd, and the main kernel checks
+//     [b S mod L]B + [a](-A) + [b](-R) == identity
+// which is [b](R' - R) == 0: since b is odd and 0 < |b| < L, that holds iff
+// R' == R (the group has order 8L; a = b h mod 8L, not just mod L, keeps the
+// torsion part of a mixed-order A exact).  R' == R is libsodium's
+// encode(R') == R bytes for canonical, decodable R; any other R is rejected
+// up front, as libsodium's compare would.  ~27 windows of doublings instead of
+// 51, and no inversion at the end; the price is a second decompression (R) and
+// a second per-lane table in the prep kernel.
+//
+// [a](-A), [b](-R): fixed signed windows of 5 bits (digits in [-16, 15], the top
+// one >= 0) against per-lane tables 0..16 x (-A) and 0..16 x (-R); the window
+// count is the wave's maximum over its lanes (26-28 in practice, at most 51).
+// [b S mod L]B = [s_lo]B + [s_hi](2^130 B): 9 signed radix-2^15 digits of each
+// half against shared tables 0..2^14 x B and 0..2^14 x 2^130 B, both added at
+// every third window (15 = 3 x 5 bits) from window 24 down.
+constexpr int kAWin = 5;                        // bits per [a](-A) / [b](-R) window
+constexpr int kAWindows = 51;                   // at most: 51 x 5 = 255 bits >= 253
+constexpr int kAEntries = 17;                   // per-lane table 0..16 x P, cached form (entry 0 = identity)
+constexpr int kBBits = 15;                      // radix 2^15 digits of the B scalar halves
+constexpr int kBSplit = 130;                    // s = s_lo + 2^130 s_hi
+constexpr int kBDigits = 9;                     // digits per half: 9 x 15 = 135 bits >= 130
 constexpr int kBEvery = kBBits / kAWin;         // a B digit every third window
-constexpr int kBEntries = (1 << (kBBits - 1)) + 1; // shared table 0..2^14 x B, affine precomp form (2 MiB)
+constexpr int kBMinWindows = kBEvery * (kBDigits - 1) + 1;  // 25: the walk reaches window 24
+constexpr int kBEntries = (1 << (kBBits - 1)) + 1; // per table 0..2^14 x base, affine precomp form (2 MiB)
+constexpr int kBTables = 2;                     // base B and base 2^130 B
 static_assert(kBBits % kAWin == 0, "B digits must land on window boundaries");
 constexpr int kCombEntries = 129;               // signer comb rows: 0..128 x 256^i B
 constexpr int kBStride = 32;                    // words per B / comb entry (30 used; 128-byte aligned)
@@ -175,10 +190,336 @@ EDV_HD void recode8(uint32_t out[8], const uint32_t s[8]) {
     out[w] = packed;
   }
 }
-// S (verify, V8): 17 signed radix-2^15 digits in [-2^14, 2^14).  V2 leaves
-// S < 2^253, so the top digit is <= 2^13 and stays inside the 0..2^14 table.
-EDV_HD void recode15(uint32_t out[8], const uint32_t s[8]) { recode_signed<kBBits, kBDigits>(out, s); }
+// 17 signed radix-2^15 digits of a scalar < 2^253 (kept for the recoding tests)
+EDV_HD void recode15(uint32_t out[8], const uint32_t s[8]) { recode_signed<kBBits, 17>(out, s); }
 EDV_HD void recode16(uint32_t out[8], const uint32_t s[8]) { recode_signed<16, 16>(out, s); }
+
+// Number of windows the packed radix-32 digits need: 1 + index of the top
+// nonzero digit (0 for a zero scalar).
+EDV_HD int digits5_windows(const uint32_t d[8]) {
+  int n = 0;
+#pragma unroll
+  for (int k = 0; k < kAWindows; k++) {
+    const int pos = kAWin * k, wi = pos >> 5, sh = pos & 31;
+    const uint64_t win = uint64_t(d[wi]) | (wi + 1 < 8 ? uint64_t(d[wi + 1]) << 32 : 0);
+    n = ((win >> sh) & 31) ? k + 1 : n;
+  }
+  return n;
+}
+
+// ------------------------------------------- 256-bit words (lattice reduction)
+EDV_HD int mx(int a, int b) { return a > b ? a : b; }
+EDV_HD bool w8_lt(const uint32_t a[8], const uint32_t b[8]) {
+  bool lt = false, eq = true;
+#pragma unroll
+  for (int i = 7; i >= 0; i--) {
+    lt = lt || (eq && a[i] < b[i]);
+    eq = eq && a[i] == b[i];
+  }
+  return lt;
+}
+EDV_HD void w8_add(uint32_t a[8], const uint32_t b[8]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c += uint64_t(a[i]) + b[i];
+    a[i] = uint32_t(c);
+    c >>= 32;
+  }
+}
+EDV_HD void w8_sub(uint32_t a[8], const uint32_t b[8]) {
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int64_t s = int64_t(a[i]) - int64_t(b[i]) + br;
+    a[i] = uint32_t(s);
+    br = s >> 32;
+  }
+}
+EDV_HD int w8_bitlen(const uint32_t a[8]) {
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) n = a[i] ? 32 * i + 32 - __builtin_clz(a[i]) : n;
+  return n;
+}
+EDV_HD double w8_to_f64(const uint32_t a[8]) {
+  double d = 0.0;
+#pragma unroll
+  for (int i = 7; i >= 0; i--) d = d * 4294967296.0 + double(a[i]);  // x 2^32 is exact; one rounding per word
+  return d;
+}
+EDV_HD void w8_shl1(uint32_t a[8]) {
+#pragma unroll
+  for (int i = 7; i > 0; i--) a[i] = (a[i] << 1) | (a[i - 1] >> 31);
+  a[0] <<= 1;
+}
+EDV_HD void w8_sar1(uint32_t a[8]) {
+#pragma unroll
+  for (int i = 0; i < 7; i++) a[i] = (a[i] >> 1) | (a[i + 1] << 31);
+  a[7] = uint32_t(int32_t(a[7]) >> 1);
+}
+EDV_HD void w8_shr1(uint32_t a[8]) {
+#pragma unroll
+  for (int i = 0; i < 7; i++) a[i] = (a[i] >> 1) | (a[i + 1] << 31);
+  a[7] >>= 1;
+}
+
+// One Euclidean division step of the lattice reduction: q = floor(r0 / r1)
+// (r0 >= r1 > 0), r0 <- r0 - q r1, t0 <- t0 - q t1 (cofactors signed, two's
+// complement mod 2^256).  q comes from a double-precision quotient of the two
+// values scaled down by 2^-44 (relative error of the doubles < 2^-49), so for
+// q < 2^31 the estimate is q or q - 1 and one masked subtraction finishes it
+// (no branch); a larger quotient takes exact binary long division.
+EDV_HD void euclid_div(uint32_t r0[8], uint32_t t0[8], const uint32_t r1[8], const uint32_t t1[8]) {
+  const double qd = __builtin_floor(w8_to_f64(r0) / w8_to_f64(r1) * (1.0 - 0x1p-44));
+  uint32_t q = 0;
+  if (qd < 2147483648.0) {
+    q = uint32_t(qd);
+    uint64_t c = 0;
+    int64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint64_t p = uint64_t(q) * r1[i] + c;
+      c = p >> 32;
+      const int64_t s = int64_t(r0[i]) - int64_t(uint32_t(p)) + br;
+      r0[i] = uint32_t(s);
+      br = s >> 32;
+    }
+  } else {
+    // binary long division over quotient bits e..0, 2^e <= qd <= q: r1 << e
+    // stays below r0, so nothing overflows
+    uint32_t d[8], v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) { d[i] = r1[i]; v[i] = t1[i]; }
+    const int e = int((__builtin_bit_cast(uint64_t, qd) >> 52) & 0x7ff) - 1023;  // floor(log2 qd), qd >= 2^31
+#pragma unroll 1
+    for (int k = 0; k < e; k++) { w8_shl1(d); w8_shl1(v); }
+#pragma unroll 1
+    for (int k = e; k >= 0; k--) {
+      if (!w8_lt(r0, d)) { w8_sub(r0, d); w8_sub(t0, v); }
+      w8_shr1(d);
+      w8_sar1(v);  // t1 2^k, sign-extended (|t1 2^e| < 2^255: exact)
+    }
+  }
+  // quotient one too small: subtract r1 once more (masked, no branch)
+  const uint32_t m = w8_lt(r0, r1) ? 0u : ~0u;
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int64_t s = int64_t(r0[i]) - int64_t(r1[i] & m) + br;
+    r0[i] = uint32_t(s);
+    br = s >> 32;
+  }
+  q -= m;  // + 1 when m = ~0
+  uint64_t c = 0;
+  int64_t bt = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t p = uint64_t(q) * t1[i] + c;
+    c = p >> 32;
+    const int64_t s = int64_t(t0[i]) - int64_t(uint32_t(p)) + bt;
+    t0[i] = uint32_t(s);
+    bt = s >> 32;
+  }
+}
+
+EDV_HD bool w8_ge128(const uint32_t r[8]) { return (r[4] | r[5] | r[6] | r[7]) != 0; }
+
+// floor(r / 2^s) for r < 2^(s + 53), as an exact double
+EDV_HD double w8_window53(const uint32_t r[8], int s) {
+  const int wi = s >> 5, b = s & 31;
+  uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    w0 = k == wi ? r[k] : w0;
+    w1 = k == wi + 1 ? r[k] : w1;
+    w2 = k == wi + 2 ? r[k] : w2;
+  }
+  const uint64_t lo = (uint64_t(w1) << 32) | w0;
+  const uint64_t v = b == 0 ? lo : ((lo >> b) | (uint64_t(w2) << (64 - b)));
+  return double(v);
+}
+// floor(a / b) for exact non-negative integers a < 2^54, 0 < b < 2^54 in doubles
+EDV_HD double fdiv_floor(double a, double b) {
+  double q = __builtin_floor(a / b);
+  const double r = __builtin_fma(-q, b, a);
+  q = r < 0 ? q - 1 : (r >= b ? q + 1 : q);
+  return q;
+}
+// (a x + b y) mod 2^256 for cofactor rows with a, b of opposite signs (or zero)
+EDV_HD void w8_lin(uint32_t out[8], const uint32_t x[8], const uint32_t y[8], int32_t a, int32_t b) {
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int64_t v = int64_t(a) * int64_t(uint64_t(x[i])) + int64_t(b) * int64_t(uint64_t(y[i])) + c;
+    out[i] = uint32_t(v);
+    c = v >> 32;
+  }
+}
+
+// One Lehmer round: Euclid simulated on the leading 53 bits of (r0, r1) in
+// doubles, quotients taken only while both ends of the truncation interval give
+// the same one (Knuth 4.5.2, Algorithm L), and only while the true remainder
+// provably stays >= 2^128, so the first remainder below 2^128 is still reached
+// by exact steps; then the cofactor matrix is applied to (r0, r1) and (t0, t1)
+// once.  About 25 bits of reduction per round for one multiword pass instead of
+// ~15 exact divisions.  Returns false if no quotient could be taken.
+EDV_HD bool lehmer_round(uint32_t r0[8], uint32_t r1[8], uint32_t t0[8], uint32_t t1[8]) {
+  const int n = w8_bitlen(r0);
+  const int s = n > 53 ? n - 53 : 0;
+  double x = w8_window53(r0, s), y = w8_window53(r1, s);
+  const double thr = __builtin_ldexp(1.0, 128 - s);
+  double A = 1, B = 0, C = 0, D = 1;
+#pragma unroll 1
+  for (int k = 0; k < 60; k++) {
+    const double yc = y + C, yd = y + D;
+    if (!(yc > 0 && yd > 0)) break;
+    const double q = fdiv_floor(x + A, yc);
+    if (q != fdiv_floor(x + B, yd)) break;
+    const double yn = x - q * y, Cn = A - q * C, Dn = B - q * D;
+    // true next remainder > (yn - |Cn| - |Dn|) 2^s; keep the cofactors < 2^30
+    if (yn - __builtin_fabs(Cn) - __builtin_fabs(Dn) < thr || __builtin_fabs(Cn) + __builtin_fabs(Dn) > 0x1p30) break;
+    A = C; B = D; C = Cn; D = Dn;
+    x = y; y = yn;
+  }
+  if (B == 0) return false;
+  const int32_t a = int32_t(A), b = int32_t(B), c = int32_t(C), d = int32_t(D);
+  uint32_t n0[8], n1[8];
+  w8_lin(n0, r0, r1, a, b);
+  w8_lin(n1, r0, r1, c, d);
+#pragma unroll
+  for (int i = 0; i < 8; i++) { r0[i] = n0[i]; r1[i] = n1[i]; }
+  w8_lin(n0, t0, t1, a, b);
+  w8_lin(n1, t0, t1, c, d);
+#pragma unroll
+  for (int i = 0; i < 8; i++) { t0[i] = n0[i]; t1[i] = n1[i]; }
+  return true;
+}
+
+EDV_HD bool w8_neg_(const uint32_t t[8]) { return t[7] >> 31; }
+EDV_HD void w8_abs(uint32_t out[8], const uint32_t t[8]) {
+  const uint32_t m = w8_neg_(t) ? ~0u : 0u;
+  uint64_t c = m & 1;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c += uint64_t(t[i] ^ m);
+    out[i] = uint32_t(c);
+    c >>= 32;
+  }
+}
+
+// The lattice reduction: (a, u, neg) with a = b h (mod 8L), b = (neg ? -u : u)
+// odd, a >= 0, both about 2^128 (Euclid on (8L, h) stopped at the first
+// remainder below 2^128: r_i = t_i h (mod 8L) throughout, and |t_i| <= 8L /
+// r_(i-1) <= 2^127 at the stop).  Consecutive cofactors are coprime, so if
+// that t_i is even its neighbours are odd; the shorter of them is taken.
+// Always a < 2^253 and u < 2^192.  Lehmer rounds take the bulk of the
+// reduction; exact divisions (two per trip, so the pairs trade places instead
+// of being copied) take the last few steps down to the threshold.
+EDV_HD void half_scalars(const uint32_t h[8], uint32_t a[8], uint32_t u[8], bool& neg) {
+  uint32_t r0[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u, 0u, 0u, 0u, 0x80000000u};  // 8L
+  uint32_t r1[8], t0[8], t1[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) { r1[i] = h[i]; t0[i] = 0; t1[i] = i == 0; }
+#pragma unroll 1
+  for (int it = 0; it < 40 && w8_bitlen(r1) > 140; it++) {
+    if (!lehmer_round(r0, r1, t0, t1)) break;
+  }
+  bool flip = false;  // the current pair is (r0, t0) rather than (r1, t1)
+  if (w8_ge128(r1)) {
+#pragma unroll 1
+    for (int it = 0; it < 200; it++) {
+      euclid_div(r0, t0, r1, t1);
+      if (!w8_ge128(r0)) { flip = true; break; }
+      euclid_div(r1, t1, r0, t0);
+      if (!w8_ge128(r1)) break;
+    }
+  }
+  if (flip) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint32_t tr = r0[i], tt = t0[i];
+      r0[i] = r1[i]; t0[i] = t1[i];
+      r1[i] = tr; t1[i] = tt;
+    }
+  }
+  // candidates: cur = (r1, t1), prev = (r0, t0); if cur's cofactor is even,
+  // next = prev - q cur (only when r1 >= 2^64, which keeps its cofactor below
+  // 2^192)
+  uint32_t u0[8], u1[8];
+  w8_abs(u0, t0);
+  w8_abs(u1, t1);
+  const bool cur_ok = u1[0] & 1, prev_ok = u0[0] & 1;
+  const int cur_len = mx(w8_bitlen(r1), w8_bitlen(u1)), prev_len = mx(w8_bitlen(r0), w8_bitlen(u0));
+  if (cur_ok && (!prev_ok || cur_len <= prev_len)) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) { a[i] = r1[i]; u[i] = u1[i]; }
+    neg = w8_neg_(t1);
+    return;
+  }
+  // prev is odd here (cur is even, or cur is longer)
+#pragma unroll
+  for (int i = 0; i < 8; i++) { a[i] = r0[i]; u[i] = u0[i]; }
+  neg = w8_neg_(t0);
+  if (!cur_ok && (r1[2] | r1[3])) {
+    euclid_div(r0, t0, r1, t1);  // (r0, t0) = next
+    w8_abs(u0, t0);
+    if (mx(w8_bitlen(r0), w8_bitlen(u0)) < prev_len) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) { a[i] = r0[i]; u[i] = u0[i]; }
+      neg = w8_neg_(t0);
+    }
+  }
+}
+
+// (u * S) mod L for u < 2^256, S < 2^256 (8 words each)
+EDV_HD void sc_mul(uint32_t out[8], const uint32_t u[8], const uint32_t s[8]) {
+  uint32_t t[16];
+  uint64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    uint64_t lo = carry, hi = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (j < 0 || j > 7) continue;
+      const uint64_t p = uint64_t(u[i]) * s[j];
+      const uint64_t x = lo + p;
+      hi += (x < lo);
+      lo = x;
+    }
+    t[k] = uint32_t(lo);
+    carry = (lo >> 32) | (hi << 32);
+  }
+  sc_reduce(out, t);
+}
+
+// B-scalar digits of s < L: word k (k < 9) = radix-2^15 digit k of s_lo = s mod
+// 2^130 in its low 16 bits and digit k of s_hi = s >> 130 in its high 16 bits,
+// both signed (two's complement in 16 bits; |d| <= 2^14, top digits >= 0).
+EDV_HD void recode_bscalar(uint32_t bw[kBDigits], const uint32_t s[8]) {
+  uint32_t lo[8], hi[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int src = i + kBSplit / 32;
+    const uint32_t w0 = src < 8 ? s[src] : 0, w1 = src + 1 < 8 ? s[src + 1] : 0;
+    hi[i] = (w0 >> (kBSplit % 32)) | (w1 << (32 - kBSplit % 32));
+    lo[i] = i < kBSplit / 32 ? s[i] : (i == kBSplit / 32 ? s[i] & ((1u << (kBSplit % 32)) - 1) : 0);
+  }
+  uint32_t dl[8], dh[8];
+  recode_signed<kBBits, kBDigits>(dl, lo);
+  recode_signed<kBBits, kBDigits>(dh, hi);
+#pragma unroll
+  for (int k = 0; k < kBDigits; k++) {
+    const int pos = kBBits * k, wi = pos >> 5, sh = pos & 31;
+    const uint64_t wl = uint64_t(dl[wi]) | (wi + 1 < 8 ? uint64_t(dl[wi + 1]) << 32 : 0);
+    const uint64_t wh = uint64_t(dh[wi]) | (wi + 1 < 8 ? uint64_t(dh[wi + 1]) << 32 : 0);
+    // sign-extend the 15-bit fields to 16 bits
+    const uint32_t el = uint32_t(int32_t(uint32_t(wl >> sh) << 17) >> 17) & 0xffffu;
+    const uint32_t eh = uint32_t(int32_t(uint32_t(wh >> sh) << 17) >> 17) & 0xffffu;
+    bw[k] = el | (eh << 16);
+  }
+}
 // shift a 256-bit little-endian word vector left by N bits (0 < N < 32)
 template <int N>
 EDV_HD void shl256(uint32_t v[8]) {
@@ -194,14 +535,19 @@ EDV_HD ge_precomp precomp_from_words(const int32_t* w) {
   return q;
 }
 
-// j * B for j in [0, 2^15], affine precomp form, written as kBStride words.
-EDV_HD void btab_entry(int32_t* o, int j) {
+// [2^shift] B
+EDV_HD ge_p3 base_point(int shift) {
   const uint32_t Bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                           0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
   ge_p3 nB;
   ge_frombytes_negate(nB, Bw);
-  const ge_p3 B{fe_neg(nB.X), nB.Y, nB.Z, fe_neg(nB.T)};
-  const ge_cached Bc = ge_p3_to_cached(B);
+  ge_p3 B{fe_neg(nB.X), nB.Y, nB.Z, fe_neg(nB.T)};
+  for (int k = 0; k < shift; k++) B = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(B)));
+  return B;
+}
+// j * base for j in [0, 2^14], affine precomp form, written as kBStride words.
+EDV_HD void btab_entry(int32_t* o, int j, const ge_p3& base) {
+  const ge_cached Bc = ge_p3_to_cached(base);
   ge_p3 acc = ge_p3_identity();
   for (int bit = kBBits - 1; bit >= 0; bit--) {
     acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
@@ -216,101 +562,160 @@ EDV_HD void btab_entry(int32_t* o, int j) {
   o[31] = 0;
 }
 
-// Phase 1 of one signature (kernel edv_prep_kernel): strictness checks V2-V4,
-// decompression V5, h = SHA-512(R || A || M) mod L (V6, V7), digit recoding and
-// the 0..16 x (-A) table (entry 0 the identity, so a zero digit needs no select).  Returns false if the signature is already rejected
-// (then hd/sd/table are unspecified).  ATab provides store(e, cached).
+// Per-lane outputs of phase 1 that phase 2 consumes.
+struct PrepDigits {
+  uint32_t da[8];        // packed signed radix-32 digits of a ([a](-A))
+  uint32_t db[8];        // packed signed radix-32 digits of |b| ([b](-R), sign folded into the R table)
+  uint32_t bw[kBDigits]; // B-scalar digit pairs (recode_bscalar)
+  int nwin;              // windows this lane needs (max over a and |b|)
+  bool negR;             // b < 0: the R digits are negated ([b](-R) = [|b|](R))
+};
+
+// 0..16 x P into a per-lane table (entry 0 the identity, so a zero digit needs
+// no select).  P comes out of a decompression affine (Z = 1, T = XY), so its
+// cached form doubles as precomp form and each further entry is a mixed
+// addition (3 field products instead of 4).
+template <class Tab>
+EDV_HD void build_table(Tab& tab, const ge_p3& P) {
+  const ge_cached c1 = ge_p3_to_cached(P);
+  const ge_precomp p1{c1.YpX, c1.YmX, c1.T2d};
+  tab.store(0, ge_cached_identity());
+  tab.store(1, c1);
+  ge_p3 cur = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(P)));
+  tab.store(2, ge_p3_to_cached(cur));
+#pragma unroll 1
+  for (int e = 3; e < kAEntries; e++) {
+    cur = ge_p1p1_to_p3(ge_madd(cur, p1));
+    tab.store(e, ge_p3_to_cached(cur));
+  }
+}
+
+// Phase 1a of one signature (kernel edv_prep_kernel, A side): strictness
+// checks V2-V4, h = SHA-512(R || A || M) mod L (V6, V7), the half-size scalars
+// (a, b), the B scalar b S mod L, digit recoding, decompression of A (V5) and
+// the 0..16 x (-A) table.  Returns false if the signature is already rejected
+// (then the digits and the table are unspecified).
 template <class ATab>
 EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen,
-                     ATab& at, uint32_t hd[8], uint32_t sd[8]) {
+                     ATab& at, PrepDigits& pd) {
   bool ok = !((S[7] & 0xF0000000u) && !sc_is_canonical(S));
   ok = ok && !has_small_order(R);
   ok = ok && ge_is_canonical(A) && !has_small_order(A);
   if (!ok) return false;
-  ge_p3 nA;
-  if (!ge_frombytes_negate(nA, A)) return false;
+  // hash and lattice first, points after: the two decompressions and tables
+  // then run one after the other with little else live (register pressure)
   uint32_t dig[16], h[8];
   hram(dig, R, A, m, mlen);
   sc_reduce(h, dig);
-  recode5(hd, h);
-  recode15(sd, S);
-  const ge_cached c1 = ge_p3_to_cached(nA);
-  // -A comes out of the decompression affine (Z = 1, T = XY), so its cached form
-  // doubles as precomp form and each further entry is a mixed addition (3 field
-  // products instead of 4: 14 products saved per signature)
-  const ge_precomp p1{c1.YpX, c1.YmX, c1.T2d};
-  at.store(0, ge_cached_identity());
-  at.store(1, c1);
-  ge_p3 cur = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(nA)));
-  at.store(2, ge_p3_to_cached(cur));
-#pragma unroll 1
-  for (int e = 3; e < kAEntries; e++) {
-    cur = ge_p1p1_to_p3(ge_madd(cur, p1));
-    at.store(e, ge_p3_to_cached(cur));
+  uint32_t a[8], u[8];
+  bool neg;
+  half_scalars(h, a, u, neg);
+  // B scalar: b S mod L with b = (neg ? -u : u)
+  uint32_t s[8];
+  sc_mul(s, u, S);
+  const uint32_t L[8] = {0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu, 0, 0, 0, 0x10000000u};
+  const bool sz = (s[0] | s[1] | s[2] | s[3] | s[4] | s[5] | s[6] | s[7]) == 0;
+  if (neg && !sz) {
+    uint32_t t[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) t[i] = L[i];
+    w8_sub(t, s);
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = t[i];
   }
+  recode_bscalar(pd.bw, s);
+  recode5(pd.da, a);
+  recode5(pd.db, u);
+  pd.nwin = mx(digits5_windows(pd.da), digits5_windows(pd.db));
+  pd.negR = neg;
+  ge_p3 nA;
+  if (!ge_frombytes_negate(nA, A)) return false;
+  build_table(at, nA);
   return true;
 }
 
-// Phase 2 (kernel edv_main_kernel): V8 R' = [h](-A) + [S]B by a joint
-// fixed-window walk, top digit first -- every lane adds at the same positions,
-// so a wave never diverges -- then V9 encode(R') == R.  51 windows of 5 bits for
-// [h](-A) (one table addition each); [S]B adds one radix-2^15 digit every third
-// window.  ATab provides load(e); BTab provides entry(j) -> precomp.
+// Phase 1b (kernel edv_prep_kernel, R side, concurrent with 1a): decompress -R
+// and its 0..16 x (-R) table.  encode(R') is canonical and a curve point's
+// encoding, so R bytes that are not canonical or decode to no point can never
+// match it (libsodium rejects them in its final compare): false.
+template <class ATab>
+EDV_HD bool prep_r(const uint32_t R[8], ATab& rt) {
+  if (!ge_is_canonical(R) || has_small_order(R)) return false;
+  ge_p3 nR;
+  if (!ge_frombytes_negate(nR, R)) return false;
+  build_table(rt, nR);
+  return true;
+}
+
+// Phase 2 (kernel edv_main_kernel): Q = [s_lo]B + [s_hi](2^130 B) + [a](-A) +
+// [|b|](-+R) by a joint fixed-window walk, top window first -- every lane adds
+// at the same positions, so a wave never diverges -- then Q == identity.
+// nwin: windows to walk (the wave's maximum; >= every lane's own count);
+// da/db are consumed from the top (shifted left 5 bits per window), bw from
+// entry kBDigits-1 down.  ATab provides load(e); BTab provides entry(t, j).
 template <class ATab, class BTab>
-EDV_HD bool main_one(const uint32_t R[8], uint32_t hd[8], uint32_t sd[8], const ATab& at, const BTab& bt) {
-  ge_p2 acc = ge_p2_identity();
-  int bphase = (kAWindows - 1) % kBEvery;  // windows until the next B digit
+EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int nwin, bool negR, const ATab& at,
+                     const ATab& rt, const BTab& bt) {
+  nwin = mx(nwin, kBMinWindows);
+  // align window nwin-1 with bits [250, 255)
 #pragma unroll 1
-  for (int w = kAWindows - 1; w >= 0; --w) {
+  for (int k = nwin; k < kAWindows; k++) {
+    shl256<kAWin>(da);
+    shl256<kAWin>(db);
+  }
+  ge_p2 acc = ge_p2_identity();
+#pragma unroll 1
+  for (int w = nwin - 1; w >= 0; --w) {
     // table reads first, so their latency hides under this window's doublings
-    const int dA = int32_t(hd[7] << 1) >> (32 - kAWin);  // digit at bits [250, 255)
-    shl256<kAWin>(hd);
-    ge_cached c = at.load(dA < 0 ? -dA : dA);
-    const bool addB = bphase == 0;
-    bphase = addB ? kBEvery - 1 : bphase - 1;
-    int dB = 0;
-    ge_precomp q;
+    const int dA = int32_t(da[7] << 1) >> (32 - kAWin);  // digit at bits [250, 255)
+    const int dR = int32_t(db[7] << 1) >> (32 - kAWin);
+    shl256<kAWin>(da);
+    shl256<kAWin>(db);
+    ge_cached ca = at.load(dA < 0 ? -dA : dA);
+    ge_cached cr = rt.load(dR < 0 ? -dR : dR);
+    const bool addB = (w % kBEvery) == 0 && w < kBMinWindows;
+    int d0 = 0, d1 = 0;
+    ge_precomp q0, q1;
     if (addB) {
-      dB = int32_t(sd[7] << 1) >> (32 - kBBits);  // digit at bits [240, 255)
-      shl256<kBBits>(sd);
-      // shift before the loads are issued: scheduled after them, the shift's
-      // temporaries landed in the loads' destination VGPRs and forced a vmcnt
-      // wait right behind the loads
+      const uint32_t pair = bw[kBDigits - 1];
+#pragma unroll
+      for (int k = kBDigits - 1; k > 0; k--) bw[k] = bw[k - 1];
+      d0 = int32_t(pair << 16) >> 16;
+      d1 = int32_t(pair) >> 16;
       sched_fence();
-      q = bt.entry(dB < 0 ? -dB : dB);
+      q0 = bt.entry(0, d0 < 0 ? -d0 : d0);
+      q1 = bt.entry(1, d1 < 0 ? -d1 : d1);
     }
     ge_p3 p3;
-    if (w == kAWindows - 1) {
+    if (w == nwin - 1) {
       p3 = ge_p3_identity();
     } else {
 #pragma unroll
       for (int d = 0; d < kAWin - 1; d++) acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
       p3 = ge_p1p1_to_p3(ge_p2_dbl(acc));
     }
-    c = ge_cached_cneg(c, dA < 0);
-    ge_p1p1 t = ge_add(p3, c);
+    p3 = ge_p1p1_to_p3(ge_add(p3, ge_cached_cneg(ca, dA < 0)));
+    ge_p1p1 t = ge_add(p3, ge_cached_cneg(cr, (dR < 0) != negR));
     if (addB) {
       p3 = ge_p1p1_to_p3(t);
-      t = ge_madd(p3, ge_precomp_cneg(q, dB < 0));
+      p3 = ge_p1p1_to_p3(ge_madd(p3, ge_precomp_cneg(q0, d0 < 0)));
+      t = ge_madd(p3, ge_precomp_cneg(q1, d1 < 0));
     }
     acc = ge_p1p1_to_p2(t);
   }
-  uint32_t enc[8];
-  ge_p2_tobytes(enc, acc);
-  bool match = true;
-#pragma unroll
-  for (int k = 0; k < 8; k++) match = match && (enc[k] == R[k]);
-  return match;
+  // identity: X = 0 and Y = Z (mod p)
+  return fe_iszero(acc.X) && fe_iszero(fe_carry32(fe_sub(acc.Y, acc.Z)));
 }
 
 // The whole verdict for one signature: true iff libsodium's verify_detached
 // would return 0.
 template <class ATab, class BTab>
 EDV_HD bool verify_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen,
-                       ATab& at, const BTab& bt) {
-  uint32_t hd[8], sd[8];
-  if (!prep_one(R, S, A, m, mlen, at, hd, sd)) return false;
-  return main_one(R, hd, sd, at, bt);
+                       ATab& at, ATab& rt, const BTab& bt) {
+  PrepDigits pd;
+  if (!prep_one(R, S, A, m, mlen, at, pd)) return false;
+  if (!prep_r(R, rt)) return false;
+  return main_one(pd.da, pd.db, pd.bw, pd.nwin, pd.negR, at, rt, bt);
 }
 
 // ------------------------------------------------ batch signing (row f-4)

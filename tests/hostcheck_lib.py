@@ -22,5 +22,8 @@ def load():
         _lib.hc_sha256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
         _lib.hc_recode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p]
         _lib.hc_btab.argtypes = [ctypes.c_void_p]
+        _lib.hc_btab_table.argtypes = [ctypes.c_int, ctypes.c_void_p]
+        _lib.hc_half_scalars.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p]
+        _lib.hc_recode_bscalar.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
         _lib.hc_verify_batch.argtypes = [ctypes.c_char_p] * 3 + [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
     return _lib

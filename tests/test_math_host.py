@@ -201,3 +201,101 @@ def test_btab_entries_are_multiples_of_B():
         assert xy2d == 2 * d * x * y % P, j
         enc = int.to_bytes(y | ((x & 1) << 255), 32, "little")
         assert enc == orc.scalarmult_base(j.to_bytes(32, "little")), j
+
+
+def test_btab_second_table_is_multiples_of_2_130_B():
+    """Table 1 of the B-scalar walk: j x 2^130 B (s = s_lo + 2^130 s_hi), against
+    the oracle's [j 2^130]B."""
+    import oracle_lib as orc
+    hc = hostcheck_lib.load()
+    n = hc.hc_btab_entries()
+    tab = (ctypes.c_int32 * (n * 32))()
+    assert hc.hc_btab_table(1, tab) == 0
+    inv2 = pow(2, P - 2, P)
+    for j in [0, 1, 2, 3, 255, 8191, 16384]:
+        e = list(tab[32 * j: 32 * j + 32])
+        ypx, ymx = val(e[0:10]) % P, val(e[10:20]) % P
+        y, x = (ypx + ymx) * inv2 % P, (ypx - ymx) * inv2 % P
+        enc = int.to_bytes(y | ((x & 1) << 255), 32, "little")
+        assert enc == orc.scalarmult_base(((j << 130) % L).to_bytes(32, "little")), j
+
+
+N8L = 8 * L
+
+
+def _half(hc, h):
+    a, u = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+    neg = hc.hc_half_scalars(h.to_bytes(32, "little"), a, u)
+    a, u = int.from_bytes(a.raw, "little"), int.from_bytes(u.raw, "little")
+    return a, (-u if neg else u)
+
+
+def test_half_scalars_lattice_reduction():
+    """The prep kernel's lattice reduction: a = b h (mod 8L), b odd (so [b]Q = 0
+    iff Q = 0 for Q in a group of order 8L), a >= 0, a < 2^253, |b| < 2^192 for
+    every h < L, and both about 2^128 for hash-like h."""
+    hc = hostcheck_lib.load()
+    r = random.Random(21)
+    edge = [0, 1, 2, 3, L - 1, L - 2, 2**128 - 1, 2**128, 2**128 + 1, 2**252, 2**252 - 1, 8, 2**64, 2**64 + 1]
+    # large partial quotients (the binary long-division path): h near N8L / 2^k and N8L * j / k
+    edge += [N8L >> k for k in (4, 40, 64, 100, 124, 130, 200) if (N8L >> k) < L]
+    edge += [(N8L >> k) + 1 for k in (40, 100, 126)]
+    edge += [(N8L * j // k) % L for j, k in ((1, 3), (2, 7), (5, 11), (1, 2**33 + 1), (7, 2**61 - 1))]
+    edge += [(2**140 * x) % L for x in (1, 3, 5)]
+    # a huge quotient after a few ordinary ones (negative cofactor at that point)
+    for k in (33, 40, 70, 110):
+        for q1 in (1, 2, 3):
+            x = N8L * 2**k // (q1 * 2**k + 1)          # N8L / h = q1 + 1/2^k
+            edge += [x % L, (x + 12345) % L]
+            x = N8L * (2**k + 1) // (2 * 2**k + 3)     # quotients 1, 1, ~2^(k-1), ...
+            edge += [x % L]
+    vals = edge + [r.randrange(L) for _ in range(20000)]
+    lens = []
+    for h in vals:
+        a, b = _half(hc, h)
+        assert 0 <= a < 2**253 and abs(b) < 2**192, hex(h)
+        assert b % 2 == 1, hex(h)
+        assert (a - b * h) % N8L == 0, hex(h)
+        lens.append(max(a.bit_length(), abs(b).bit_length()))
+    rand = sorted(lens[len(edge):])
+    assert rand[len(rand) // 2] <= 128 and rand[-1] <= 142, (rand[len(rand) // 2], rand[-1])
+
+
+def test_recode_bscalar_digit_pairs():
+    """B-scalar digit pairs: s = sum d_lo,k 2^(15k) + 2^130 sum d_hi,k 2^(15k),
+    |d| <= 2^14 (indexes the 0..2^14 tables), top digits >= 0."""
+    hc = hostcheck_lib.load()
+    r = random.Random(22)
+    out = (ctypes.c_uint32 * 9)()
+    vals = [0, 1, L - 1, 2**130 - 1, 2**130, 2**252, 2**129 + 2**128] + [r.randrange(L) for _ in range(3000)]
+    for s in vals:
+        hc.hc_recode_bscalar(s.to_bytes(32, "little"), out)
+        lo = [((w & 0xffff) ^ 0x8000) - 0x8000 for w in out]
+        hi = [((w >> 16) ^ 0x8000) - 0x8000 for w in out]
+        assert all(abs(d) <= 2**14 for d in lo + hi)
+        assert lo[-1] >= 0 and hi[-1] >= 0
+        v = sum(d << (15 * k) for k, d in enumerate(lo)) + (sum(d << (15 * k) for k, d in enumerate(hi)) << 130)
+        assert v == s, hex(s)
+
+
+def test_kernel_algorithm_on_cpu_matches_libsodium_corpus_slice():
+    """The kernel algorithm (half-size scalars) on the CPU against libsodium's
+    committed verdict bits for the first 12,000 requests of the C2 and C4
+    corpora (5 % damaged: flipped R/S/A/message bits, S >= L, small-order and
+    non-canonical points)."""
+    import json
+    import os
+    import numpy as np
+    import oracle_lib as orc
+    hc = hostcheck_lib.load()
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    meta = json.load(open(os.path.join(gdir, "corpus_bitmask.json")))
+    for name, n in (("c2_256B", 12000), ("c4_var", 4000)):
+        cfg = meta["corpora"][name]
+        sigs, pks, msgs, off = orc.corpus(cfg["seed"], 0, n, cfg["mode"], cfg["invalid_permille"])
+        bits = np.fromfile(os.path.join(gdir, "corpus_%s.bits" % name), dtype=np.uint8)
+        want = np.unpackbits(bits[:n // 8], bitorder="little")
+        acc = ctypes.create_string_buffer(n)
+        hc.hc_verify_batch(sigs.tobytes(), pks.tobytes(), msgs.tobytes(), off.ctypes.data, n, acc)
+        got = np.frombuffer(acc.raw, dtype=np.uint8)
+        assert np.array_equal(got, want), (name, np.nonzero(got != want)[0][:10])
