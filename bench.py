@@ -46,8 +46,12 @@ from indy_plenum_amd import edv, shard, workload  # noqa: E402
 
 # Algorithmic INT32 work per verify:
 #   W(m) = 217,600 + 5,500 * ceil((m + 81) / 128)   (3,400 GF(p) mul/sq x 64 u32 mul-adds + SHA-512 blocks)
-# split by kernel: main = V8 loop + V9 encode = (2,737 + 267) x 64; prep = the rest.
-MAIN_OPS = (2737 + 267) * 64
+# The verify path is two launches per chunk (edv_prep_kernel, edv_main_kernel);
+# the roofline prices the whole path: W(m) per verify over the sum of both
+# kernels' HIP-event times.  (Round 1 priced the main kernel alone at
+# (2,737 + 267) x 64 ops; with half-size scalars part of that work moved into
+# prep and the rest shrank, so a per-kernel split of W would no longer mean
+# anything.)
 C3_TOTAL = 16777216
 
 
@@ -66,34 +70,38 @@ def kernel_source_hash():
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
 
-def pmc_figures(kernel, batch, msg_len, kernel_ms):
-    """Counter-derived figures for `kernel` from the committed rocprofv3 PMC
-    summary (tools/pmc_summary.py), only if it was measured on these exact kernel
-    sources at the default C2 shape; else (None, reason)."""
+def pmc_figures(kernels, batch, msg_len, kernel_ms):
+    """Counter-derived figures for the verify path (`kernels`, summed) from the
+    committed rocprofv3 PMC summary (tools/pmc_summary.py), only if it was
+    measured on these exact kernel sources at the default C2 shape; else
+    (None, reason).  kernel_ms: the summed HIP-event time of those kernels."""
     if batch != 65536 or msg_len != 256 or not os.path.exists(PMC_SUMMARY):
         return None, "no PMC summary for this shape"
     with open(PMC_SUMMARY) as f:
         s = json.load(f)
     if s.get("kernel_source_sha256") != kernel_source_hash():
         return None, "PMC summary is stale (kernel sources changed since it was measured)"
-    k = s["kernels"].get(kernel)
-    if not k:
+    ks = [s["kernels"].get(k) for k in kernels]
+    if not all(ks):
         return None, "kernel not in PMC summary"
-    c = k["counters"]
-    out = {"traffic": k.get("hbm_bytes_per_launch"),
-           "traffic_source": "%s: 2 x FETCH_SIZE + WRITE_SIZE per launch (gfx950 correction; Infinity-Cache "
-                             "(MALL) hits included, so an upper bound on DRAM bytes)" % os.path.relpath(PMC_SUMMARY, ROOT)}
-    if "SQ_INSTS_VALU" in c and c.get("SQ_WAVES"):
-        lane_ops = c["SQ_INSTS_VALU"] * 64  # one lane-op per active lane per VALU wave-instruction
+    out = {"traffic": sum(k.get("hbm_bytes_per_launch", 0.0) for k in ks),
+           "traffic_source": "%s: 2 x FETCH_SIZE + WRITE_SIZE per launch, prep + main (gfx950 correction; "
+                             "Infinity-Cache (MALL) hits included, so an upper bound on DRAM bytes)"
+                             % os.path.relpath(PMC_SUMMARY, ROOT)}
+    cs = [k["counters"] for k in ks]
+    if all("SQ_INSTS_VALU" in c for c in cs):
+        valu = sum(c["SQ_INSTS_VALU"] for c in cs)  # wave-instructions per launch pair
+        lane_ops = valu * 64  # one lane-op per active lane per VALU wave-instruction
         out.update({
-            "valu_insts_per_verify": k["valu_insts_per_wave"],  # one signature per lane: per-wave count = per verify
-            "valu_int64_insts_per_verify": c.get("SQ_INSTS_VALU_INT64", 0.0) / c["SQ_WAVES"],
-            "valu_int32_insts_per_verify": c.get("SQ_INSTS_VALU_INT32", 0.0) / c["SQ_WAVES"],
+            "valu_insts_per_verify": valu / batch,  # one signature per lane in every side
+            "valu_int64_insts_per_verify": sum(c.get("SQ_INSTS_VALU_INT64", 0.0) for c in cs) / batch,
+            "valu_int32_insts_per_verify": sum(c.get("SQ_INSTS_VALU_INT32", 0.0) for c in cs) / batch,
             "measured_valu_lane_ops_per_s": lane_ops / (kernel_ms * 1e-3),
             "measured_valu_frac_of_issue_peak": lane_ops / (kernel_ms * 1e-3) / PEAK_INT32,
-            "valu_busy": k.get("valu_busy"),
-            "wave_cycle_split": k.get("wave_cycle_split"),
-            "pmc_gpu_busy_cycles": k.get("gpu_busy_cycles"),
+            "per_kernel": {name: {"valu_insts_per_wave": k.get("valu_insts_per_wave"), "waves": k["counters"].get("SQ_WAVES"),
+                                  "valu_busy": k.get("valu_busy"), "wave_cycle_split": k.get("wave_cycle_split"),
+                                  "hbm_bytes_per_launch": k.get("hbm_bytes_per_launch")}
+                           for name, k in zip(kernels, ks)},
         })
     return out, None
 
@@ -414,17 +422,18 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
-    achieved = MAIN_OPS * pn / (main_ms * 1e-3)
-    pmc, why = pmc_figures("edv_main_kernel", n, args.msg_len, main_ms)
-    whole = w_total(args.msg_len) * pn / ((prep_ms + main_ms) * 1e-3)
-    roofline = {"bound": "valu_int32", "kernel": "edv_main_kernel",
+    path_ms = prep_ms + main_ms
+    ops = w_total(args.msg_len) * pn
+    achieved = ops / (path_ms * 1e-3)
+    pmc, why = pmc_figures(["edv_prep_kernel", "edv_main_kernel"], n, args.msg_len, path_ms)
+    roofline = {"bound": "valu_int32", "kernel": "edv_prep_kernel + edv_main_kernel (the verify path, one launch each)",
                 "achieved": achieved / 1e12, "peak": PEAK_INT32 / 1e12, "unit": "TOP/s",
-                "frac": achieved / PEAK_INT32, "traffic": None, "traffic_unit": "bytes/launch",
+                "frac": achieved / PEAK_INT32, "traffic": None, "traffic_unit": "bytes/launch pair",
                 "traffic_source": why, "algorithmic_bytes": (64 + 32 + args.msg_len + 8 + 1) * pn,
-                "ops_per_launch": MAIN_OPS * pn, "kernel_ms": main_ms, "prep_kernel_ms": prep_ms,
-                "whole_path_frac": whole / PEAK_INT32, "vop2_issue_peak": PEAK_VOP2 / 1e12,
-                "convention": "achieved = SURVEY 8d ops (main kernel: (2,737 + 267) x 64 per verify) / HIP-event "
-                              "kernel time; peak = 256 CU x 64 lanes x 2.4 GHz (4-cycle VOP3 issue)"}
+                "ops_per_launch": ops, "kernel_ms": path_ms, "prep_kernel_ms": prep_ms, "main_kernel_ms": main_ms,
+                "vop2_issue_peak": PEAK_VOP2 / 1e12,
+                "convention": "achieved = SURVEY 8d W(m) INT32 ops per verify x verifies / (prep + main HIP-event "
+                              "kernel time); peak = 256 CU x 64 lanes x 2.4 GHz (4-cycle VOP3 issue)"}
     if pmc:
         roofline.update(pmc)
     out = {

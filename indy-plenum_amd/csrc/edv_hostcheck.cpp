@@ -14,8 +14,11 @@ using namespace edv;
 namespace {
 struct HostATab {
   ge_cached t[kAEntries];
+  int staged = 0;
   void store(int e, const ge_cached& c) { t[e] = c; }
   ge_cached load(int e) const { return t[e]; }
+  void stage(int e) { staged = e; }
+  ge_cached fetch() const { return t[staged]; }
 };
 struct HostBTab {
   std::vector<int32_t> w;
@@ -26,6 +29,13 @@ struct HostBTab {
     }
   }
   ge_precomp entry(int t, int j) const { return precomp_from_words(w.data() + (t * kBEntries + j) * kBStride); }
+};
+// the main loop's staged view of the B tables
+struct HostBStage {
+  const HostBTab& b;
+  int j[kBTables] = {0, 0};
+  void stage(int t, int e) { j[t] = e; }
+  ge_precomp fetch(int t) const { return b.entry(t, j[t]); }
 };
 struct HostComb {
   std::vector<int32_t> w;
@@ -161,7 +171,8 @@ int hc_verify_batch(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs
     std::vector<uint8_t> buf(mlen + 32, 0);
     if (mlen) memcpy(buf.data() + 16, msgs + off[i], mlen);
     HostATab at, rt;
-    accept[i] = verify_one(R, S, A, buf.data() + 16, mlen, at, rt, bt) ? 1 : 0;
+    HostBStage bs{bt};
+    accept[i] = verify_one(R, S, A, buf.data() + 16, mlen, at, rt, bs) ? 1 : 0;
   }
   return 0;
 }

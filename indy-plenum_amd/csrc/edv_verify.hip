@@ -46,8 +46,8 @@ constexpr uint64_t kChunkDefault = uint64_t(1) << 18;  // signatures per prep/ma
 //   rtab[680 * i + w]  the same for its 0..16 x (-+R) table
 //   dig[w * cap + i]   w 0..7: packed radix-32 digits of a, 8..15: of |b|,
 //                      16..24: B-scalar digit pairs, 25: windows needed
-//   alive[i]           1 if the A-side prep checks passed; alive[cap + i]: the R side
-//                      (the main kernel skips lanes where either is 0)
+//   alive[k cap + i]   1 if prep side k (0 hash, 1 A, 2 R) passed for slot i (the
+//                      main kernel skips lanes where any side failed)
 struct ChunkState {
   int32_t* atab;
   int32_t* rtab;
@@ -128,6 +128,65 @@ struct GlobalBTab {
   }
 };
 
+// The main kernel's views of the tables: stage() copies the entry a lane needs
+// this window from global memory straight into the wave's LDS slice
+// (global_load_lds_dwordx4: 64 lanes x 16 B per instruction, lane-linear), so
+// nothing of it sits in registers during the window's doublings; fetch()
+// waits for the copies and reads the lane's 16-byte pieces back.  Per wave:
+// A 10 KiB + R 10 KiB + two B entries 8 KiB each = 36 KiB; 144 KiB per
+// 256-thread workgroup (one workgroup per CU at 64k signatures).
+constexpr int kLdsAWords = 10 * 256;  // one cached entry: 10 pieces of 64 lanes x 4 words
+constexpr int kLdsBWords = 8 * 256;   // one B entry: 8 pieces (words 30, 31 are padding)
+constexpr int kLdsWaveWords = 2 * kLdsAWords + kBTables * kLdsBWords;
+__device__ __forceinline__ void wait_staged() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+struct LdsATab {
+  const int32_t* slot;  // this lane's table in global memory
+  int32_t* lds;         // the wave's LDS region for this table
+  int lane;
+  __device__ __forceinline__ void stage(int e) {
+    const int32_t* g = slot + e * 40;
+#pragma unroll
+    for (int q = 0; q < 10; q++)
+      __builtin_amdgcn_global_load_lds(const_cast<int32_t*>(g + 4 * q), lds + q * 256, 16, 0, 0);
+  }
+  __device__ __forceinline__ ge_cached fetch() {
+    wait_staged();
+    int32_t t[40];
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+      const int4 v = reinterpret_cast<const int4*>(lds + q * 256)[lane];
+      t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
+    }
+    ge_cached c;
+#pragma unroll
+    for (int l = 0; l < 10; l++) {
+      c.YpX.v[l] = t[l]; c.YmX.v[l] = t[10 + l]; c.Z.v[l] = t[20 + l]; c.T2d.v[l] = t[30 + l];
+    }
+    return c;
+  }
+};
+struct LdsBTab {
+  const int32_t* w;  // both shared tables
+  int32_t* lds;      // kBTables x kLdsBWords
+  int lane;
+  __device__ __forceinline__ void stage(int tb, int j) {
+    const int32_t* g = w + (tb * kBEntries + j) * kBStride;
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+      __builtin_amdgcn_global_load_lds(const_cast<int32_t*>(g + 4 * q), lds + tb * kLdsBWords + q * 256, 16, 0, 0);
+  }
+  __device__ __forceinline__ ge_precomp fetch(int tb) {
+    wait_staged();
+    int32_t t[32];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int4 v = reinterpret_cast<const int4*>(lds + tb * kLdsBWords + q * 256)[lane];
+      t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
+    }
+    return precomp_from_words(t);
+  }
+};
+
 __device__ __forceinline__ void load_words(uint32_t* out, const uint32_t* p, int n4) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
@@ -137,28 +196,33 @@ __device__ __forceinline__ void load_words(uint32_t* out, const uint32_t* p, int
   }
 }
 
-// Phase 1: V2-V7, half-size scalars, digit recoding and the A table (even
-// workgroups), R decompression and the R table (odd workgroups).  The two
-// halves share no data, so they run side by side: two waves per SIMD at 64k
-// signatures instead of one, each hiding the other's latencies.
-__device__ __forceinline__ void prep_r_side(const VerifyArgs& a, uint64_t j) {
+// Phase 1 in three independent sides, interleaved by workgroup (block b runs
+// side b % 3 of slots [(b / 3) 256, +256)): 0 = V2-V4 checks, V6/V7 hash,
+// half-size scalars and digits; 1 = decompress A, 0..16 x (-A) table; 2 = the
+// same for R.  They share no data, so they run side by side (three waves per
+// SIMD at 64k signatures where one kernel per side would leave one wave each
+// to hide its own latencies), and the two exponentiations no longer sit
+// behind the hash in one lane.
+__device__ __forceinline__ void prep_point_side(const VerifyArgs& a, uint64_t j, int side) {
   if (j >= a.n) return;
   const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
-  uint32_t R[8];
-  load_words(R, a.sigs + 16 * i, 2);
-  GlobalATab rt{a.st.rtab + j * kAWords};
-  const bool ok = prep_r(R, rt);
-  a.st.alive[a.st.cap + j] = ok ? 1 : 0;
+  uint32_t P[8];
+  if (side == 1) load_words(P, a.pks + 8 * i, 2);
+  else load_words(P, a.sigs + 16 * i, 2);
+  GlobalATab tab{(side == 1 ? a.st.atab : a.st.rtab) + j * kAWords};
+  const bool ok = prep_point(P, tab);
+  a.st.alive[side * a.st.cap + j] = ok ? 1 : 0;
   if (!ok) a.accept[i] = 0;
 }
 #ifndef EDV_PREP_WAVES
-#define EDV_PREP_WAVES 2  // minimum waves per SIMD the prep kernel's register budget must allow
+#define EDV_PREP_WAVES 3  // minimum waves per SIMD the prep kernel's register budget must allow (three sides)
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EDV_PREP_WAVES, 8))) void edv_prep_kernel(
     VerifyArgs a) {
-  const uint64_t j = uint64_t(blockIdx.x >> 1) * kBlock + threadIdx.x;  // slot within the chunk
-  if (blockIdx.x & 1) {
-    prep_r_side(a, j);
+  const int side = int(blockIdx.x % 3);
+  const uint64_t j = uint64_t(blockIdx.x / 3) * kBlock + threadIdx.x;  // slot within the chunk
+  if (side != 0) {
+    prep_point_side(a, j, side);
     return;
   }
   if (j >= a.n) return;
@@ -168,9 +232,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EDV_PREP
   load_words(S, a.sigs + 16 * i + 8, 2);
   load_words(A, a.pks + 8 * i, 2);
   const uint64_t o0 = a.off[i] - a.msg_base, o1 = a.off[i + 1] - a.msg_base;
-  GlobalATab at{a.st.atab + j * kAWords};
   PrepDigits pd;
-  const bool ok = prep_one(R, S, A, a.msgs + o0, o1 - o0, at, pd);
+  const bool ok = prep_one(R, S, A, a.msgs + o0, o1 - o0, pd);
   a.st.alive[j] = ok ? 1 : 0;
   if (ok) {
     uint32_t* d = a.st.dig + j;
@@ -191,8 +254,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EDV_PREP
 // Phase 2: V8 multi-scalar walk and the identity check.  The window count is
 // the wave's maximum over its live lanes, so the loop stays wave-uniform.
 __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
+  __shared__ int32_t lds_main[(kBlock / 64) * kLdsWaveWords];
   const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-  const bool live = j < a.n && a.st.alive[j] && a.st.alive[a.st.cap + j];
+  const bool live = j < a.n && a.st.alive[j] && a.st.alive[a.st.cap + j] && a.st.alive[2 * a.st.cap + j];
   const uint32_t* d = a.st.dig + j;
   const uint64_t cap = a.st.cap;
   const uint32_t wf = live ? d[uint64_t(kDigNwin) * cap] : 0;
@@ -222,8 +286,10 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   }
 #pragma unroll
   for (int k = 0; k < kBDigits; k++) bw[k] = uint32_t(opaque_i32(int32_t(bw[k])));
-  const GlobalATab at{a.st.atab + j * kAWords}, rt{a.st.rtab + j * kAWords};
-  const GlobalBTab bt{a.btab};
+  int32_t* wl = lds_main + (threadIdx.x >> 6) * kLdsWaveWords;
+  const int lane = int(threadIdx.x & 63);
+  LdsATab at{a.st.atab + j * kAWords, wl, lane}, rt{a.st.rtab + j * kAWords, wl + kLdsAWords, lane};
+  LdsBTab bt{a.btab, wl + 2 * kLdsAWords, lane};
   a.accept[i] = main_one(da, db, bw, nwin, (wf >> 8) & 1, at, rt, bt) ? 1 : 0;
 }
 
@@ -413,7 +479,7 @@ struct ChunkBufs {
   DevBuf perm, bucket_ctr;  // length-bucket permutation of a chunk; histogram + cursors (one set per stream)
   int ensure(uint64_t chunk) {
     if (atab.ensure(chunk * kAWords * 4) || rtab.ensure(chunk * kAWords * 4) || dig.ensure(chunk * kDigWords * 4) ||
-        alive.ensure(2 * chunk) ||
+        alive.ensure(3 * chunk) ||
         perm.ensure(chunk * 4) || bucket_ctr.ensure(uint64_t(kQ) * 2 * kBuckets * 4))
       return EDV_E_OOM;
     return 0;
@@ -574,7 +640,7 @@ int launch_prep(uint32_t* ctr, const VerifyArgs& va, const uint64_t* d_off, bool
                                                                      const_cast<uint32_t*>(va.st.perm));
     HIPOK(hipGetLastError(), "bucket launch");
   }
-  edv_prep_kernel<<<dim3(2 * blocks), dim3(kBlock), 0, s>>>(va);  // A and R sides
+  edv_prep_kernel<<<dim3(3 * blocks), dim3(kBlock), 0, s>>>(va);  // hash, A and R sides
   HIPOK(hipGetLastError(), "prep launch");
   return 0;
 }
@@ -1177,7 +1243,7 @@ int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uin
                                                                                const_cast<uint32_t*>(va.st.perm));
     }
     HIPOK(hipEventRecord(ev.e[0], c->stream), "record");
-    edv_prep_kernel<<<dim3(2 * blocks), dim3(kBlock), 0, c->stream>>>(va);
+    edv_prep_kernel<<<dim3(3 * blocks), dim3(kBlock), 0, c->stream>>>(va);
     HIPOK(hipEventRecord(ev.e[1], c->stream), "record");
     edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(va);
     HIPOK(hipEventRecord(ev.e[2], c->stream), "record");

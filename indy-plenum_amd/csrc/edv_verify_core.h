@@ -590,14 +590,12 @@ EDV_HD void build_table(Tab& tab, const ge_p3& P) {
   }
 }
 
-// Phase 1a of one signature (kernel edv_prep_kernel, A side): strictness
-// checks V2-V4, h = SHA-512(R || A || M) mod L (V6, V7), the half-size scalars
-// (a, b), the B scalar b S mod L, digit recoding, decompression of A (V5) and
-// the 0..16 x (-A) table.  Returns false if the signature is already rejected
-// (then the digits and the table are unspecified).
-template <class ATab>
+// Phase 1, hash side (kernel edv_prep_kernel): strictness checks V2-V4,
+// h = SHA-512(R || A || M) mod L (V6, V7), the half-size scalars (a, b), the B
+// scalar b S mod L and the digit recoding.  Returns false if the signature is
+// already rejected (then the digits are unspecified).
 EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen,
-                     ATab& at, PrepDigits& pd) {
+                     PrepDigits& pd) {
   bool ok = !((S[7] & 0xF0000000u) && !sc_is_canonical(S));
   ok = ok && !has_small_order(R);
   ok = ok && ge_is_canonical(A) && !has_small_order(A);
@@ -628,22 +626,21 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
   recode5(pd.db, u);
   pd.nwin = mx(digits5_windows(pd.da), digits5_windows(pd.db));
   pd.negR = neg;
-  ge_p3 nA;
-  if (!ge_frombytes_negate(nA, A)) return false;
-  build_table(at, nA);
   return true;
 }
 
-// Phase 1b (kernel edv_prep_kernel, R side, concurrent with 1a): decompress -R
-// and its 0..16 x (-R) table.  encode(R') is canonical and a curve point's
-// encoding, so R bytes that are not canonical or decode to no point can never
-// match it (libsodium rejects them in its final compare): false.
+// Phase 1, point sides (kernel edv_prep_kernel, concurrent with the hash
+// side): decompress -P and build its 0..16 x (-P) table, for P = A (V4, V5:
+// libsodium's checks on the key) and for P = R.  encode(R') is canonical and a
+// curve point's encoding, so R bytes that are non-canonical, of small order
+// (libsodium's blocklist) or decode to no point can never pass: the same three
+// checks reject them.  Returns false on rejection.
 template <class ATab>
-EDV_HD bool prep_r(const uint32_t R[8], ATab& rt) {
-  if (!ge_is_canonical(R) || has_small_order(R)) return false;
-  ge_p3 nR;
-  if (!ge_frombytes_negate(nR, R)) return false;
-  build_table(rt, nR);
+EDV_HD bool prep_point(const uint32_t P[8], ATab& tab) {
+  if (!ge_is_canonical(P) || has_small_order(P)) return false;
+  ge_p3 nP;
+  if (!ge_frombytes_negate(nP, P)) return false;
+  build_table(tab, nP);
   return true;
 }
 
@@ -652,10 +649,11 @@ EDV_HD bool prep_r(const uint32_t R[8], ATab& rt) {
 // at the same positions, so a wave never diverges -- then Q == identity.
 // nwin: windows to walk (the wave's maximum; >= every lane's own count);
 // da/db are consumed from the top (shifted left 5 bits per window), bw from
-// entry kBDigits-1 down.  ATab provides load(e); BTab provides entry(t, j).
+// entry kBDigits-1 down.  ATab provides stage(e) then fetch() -> cached entry e;
+// BTab stage(t, j) then fetch(t) -> entry j of table t.
 template <class ATab, class BTab>
-EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int nwin, bool negR, const ATab& at,
-                     const ATab& rt, const BTab& bt) {
+EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int nwin, bool negR, ATab& at, ATab& rt,
+                     BTab& bt) {
   nwin = mx(nwin, kBMinWindows);
   // align window nwin-1 with bits [250, 255)
 #pragma unroll 1
@@ -666,25 +664,24 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
   ge_p2 acc = ge_p2_identity();
 #pragma unroll 1
   for (int w = nwin - 1; w >= 0; --w) {
-    // table reads first, so their latency hides under this window's doublings
+    // stage(...) starts this window's table reads (on the GPU: straight into
+    // LDS, no registers held), fetch() picks them up after the doublings
     const int dA = int32_t(da[7] << 1) >> (32 - kAWin);  // digit at bits [250, 255)
     const int dR = int32_t(db[7] << 1) >> (32 - kAWin);
     shl256<kAWin>(da);
     shl256<kAWin>(db);
-    ge_cached ca = at.load(dA < 0 ? -dA : dA);
-    ge_cached cr = rt.load(dR < 0 ? -dR : dR);
+    at.stage(dA < 0 ? -dA : dA);
+    rt.stage(dR < 0 ? -dR : dR);
     const bool addB = (w % kBEvery) == 0 && w < kBMinWindows;
     int d0 = 0, d1 = 0;
-    ge_precomp q0, q1;
     if (addB) {
       const uint32_t pair = bw[kBDigits - 1];
 #pragma unroll
       for (int k = kBDigits - 1; k > 0; k--) bw[k] = bw[k - 1];
       d0 = int32_t(pair << 16) >> 16;
       d1 = int32_t(pair) >> 16;
-      sched_fence();
-      q0 = bt.entry(0, d0 < 0 ? -d0 : d0);
-      q1 = bt.entry(1, d1 < 0 ? -d1 : d1);
+      bt.stage(0, d0 < 0 ? -d0 : d0);
+      bt.stage(1, d1 < 0 ? -d1 : d1);
     }
     ge_p3 p3;
     if (w == nwin - 1) {
@@ -694,12 +691,12 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
       for (int d = 0; d < kAWin - 1; d++) acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
       p3 = ge_p1p1_to_p3(ge_p2_dbl(acc));
     }
-    p3 = ge_p1p1_to_p3(ge_add(p3, ge_cached_cneg(ca, dA < 0)));
-    ge_p1p1 t = ge_add(p3, ge_cached_cneg(cr, (dR < 0) != negR));
+    p3 = ge_p1p1_to_p3(ge_add(p3, ge_cached_cneg(at.fetch(), dA < 0)));
+    ge_p1p1 t = ge_add(p3, ge_cached_cneg(rt.fetch(), (dR < 0) != negR));
     if (addB) {
       p3 = ge_p1p1_to_p3(t);
-      p3 = ge_p1p1_to_p3(ge_madd(p3, ge_precomp_cneg(q0, d0 < 0)));
-      t = ge_madd(p3, ge_precomp_cneg(q1, d1 < 0));
+      p3 = ge_p1p1_to_p3(ge_madd(p3, ge_precomp_cneg(bt.fetch(0), d0 < 0)));
+      t = ge_madd(p3, ge_precomp_cneg(bt.fetch(1), d1 < 0));
     }
     acc = ge_p1p1_to_p2(t);
   }
@@ -711,10 +708,10 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
 // would return 0.
 template <class ATab, class BTab>
 EDV_HD bool verify_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen,
-                       ATab& at, ATab& rt, const BTab& bt) {
+                       ATab& at, ATab& rt, BTab& bt) {
   PrepDigits pd;
-  if (!prep_one(R, S, A, m, mlen, at, pd)) return false;
-  if (!prep_r(R, rt)) return false;
+  if (!prep_one(R, S, A, m, mlen, pd)) return false;
+  if (!prep_point(A, at) || !prep_point(R, rt)) return false;
   return main_one(pd.da, pd.db, pd.bw, pd.nwin, pd.negR, at, rt, bt);
 }
 
