@@ -93,9 +93,11 @@ def pmc_figures(kernels, batch, msg_len, kernel_ms):
         valu = sum(c["SQ_INSTS_VALU"] for c in cs)  # wave-instructions per launch pair
         lane_ops = valu * 64  # one lane-op per active lane per VALU wave-instruction
         out.update({
-            "valu_insts_per_verify": valu / batch,  # one signature per lane in every side
-            "valu_int64_insts_per_verify": sum(c.get("SQ_INSTS_VALU_INT64", 0.0) for c in cs) / batch,
-            "valu_int32_insts_per_verify": sum(c.get("SQ_INSTS_VALU_INT32", 0.0) for c in cs) / batch,
+            # a verify is one lane in each kernel (and in each prep side): per-lane
+            # instructions = wave-instructions x 64 lanes / verifies
+            "valu_insts_per_verify": valu * 64 / batch,
+            "valu_int64_insts_per_verify": sum(c.get("SQ_INSTS_VALU_INT64", 0.0) for c in cs) * 64 / batch,
+            "valu_int32_insts_per_verify": sum(c.get("SQ_INSTS_VALU_INT32", 0.0) for c in cs) * 64 / batch,
             "measured_valu_lane_ops_per_s": lane_ops / (kernel_ms * 1e-3),
             "measured_valu_frac_of_issue_peak": lane_ops / (kernel_ms * 1e-3) / PEAK_INT32,
             "per_kernel": {name: {"valu_insts_per_wave": k.get("valu_insts_per_wave"), "waves": k["counters"].get("SQ_WAVES"),
