@@ -1,0 +1,123 @@
+// edv_kernels.h -- what the prep kernel (edv_prep.hip) and the main kernel and
+// host runtime (edv_verify.hip) share: the per-chunk state layout, the kernel
+// arguments, the per-signature table view used by the prep kernel, and the
+// prep launch entry point.  Two translation units so the prep kernel is built
+// without the scheduling fences of the field arithmetic (edv_math.h
+// sched_fence): they keep the main kernel's registers in check, while the
+// prep kernel's serial exponentiations and table chain run faster when LLVM
+// may interleave independent products (measured: prep -7 %, main +3 % with
+// the fences removed everywhere, profiles/r02/ab_fence_s23.jsonl).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "edv_verify_core.h"
+
+namespace edv {
+
+constexpr int kBlock = 256;
+constexpr int kAWords = kAEntries * 40;   // cached point = 4 x 10 limbs (680 words = 2,720 B)
+// dig words per signature: da (8), db (8), B digit pairs (9), window count (1)
+constexpr int kDigWords = 8 + 8 + kBDigits + 1;
+constexpr int kDigB = 16, kDigNwin = 16 + kBDigits;
+constexpr uint64_t kChunkDefault = uint64_t(1) << 18;  // signatures per prep/main launch pair
+
+// Per-chunk state handed from the prep kernel to the main kernel, SoA so every
+// wave-wide load/store touches 64 consecutive words:
+//   atab[680 * i + w]  word w (0..679) of signature i's 0..16 x (-A) table
+//   rtab[680 * i + w]  the same for its 0..16 x (-+R) table
+//   dig[w * cap + i]   w 0..7: packed radix-32 digits of a, 8..15: of |b|,
+//                      16..24: B-scalar digit pairs, 25: windows needed
+//   alive[k cap + i]   1 if prep side k (0 hash, 1 A, 2 R) passed for slot i (the
+//                      main kernel skips lanes where any side failed)
+struct ChunkState {
+  int32_t* atab;
+  int32_t* rtab;
+  uint32_t* dig;
+  uint8_t* alive;
+  uint64_t cap;
+  const uint32_t* perm;   // slot j -> request base + perm[j] (length buckets); null = identity
+};
+
+struct VerifyArgs {
+  const uint32_t* sigs;   // n x 16 words
+  const uint32_t* pks;    // n x 8 words
+  const uint8_t* msgs;
+  const uint64_t* off;    // n + 1
+  uint64_t msg_base;
+  uint64_t base;          // first signature of this chunk
+  uint64_t n;             // signatures in this chunk
+  uint8_t* accept;        // indexed by global signature index
+  ChunkState st;
+  const int32_t* btab;    // kBTables x kBEntries x kBStride
+};
+
+// Per-signature A table in HBM, signature-major: signature i's 360 words are
+// contiguous at slot = atab + 360*i, so a lane's digit-dependent gather reads
+// 160 contiguous bytes (10 x 16-byte loads) instead of touching one line per
+// word for every distinct digit in the wave (the word-major layout measured
+// 39 KB of L2-miss traffic per verify, 8x the useful bytes).
+struct GlobalATab {
+  int32_t* slot;
+  // one entry = 40 contiguous words (160 B, 16-byte aligned): ten 16-byte stores
+  __device__ __forceinline__ void store(int e, const ge_cached& c) const {
+    int32_t t[40];
+#pragma unroll
+    for (int l = 0; l < 10; l++) {
+      t[l] = c.YpX.v[l]; t[10 + l] = c.YmX.v[l]; t[20 + l] = c.Z.v[l]; t[30 + l] = c.T2d.v[l];
+    }
+    int4* p = reinterpret_cast<int4*>(slot + e * 40);
+#pragma unroll
+    for (int q = 0; q < 10; q++) p[q] = make_int4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
+  }
+  __device__ __forceinline__ ge_cached load(int e) const {
+    const int4* p = reinterpret_cast<const int4*>(slot + e * 40);
+    int32_t t[40];
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+      const int4 v = p[q];
+      t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
+    }
+    ge_cached c;
+#pragma unroll
+    for (int l = 0; l < 10; l++) {
+      c.YpX.v[l] = t[l]; c.YmX.v[l] = t[10 + l]; c.Z.v[l] = t[20 + l]; c.T2d.v[l] = t[30 + l];
+    }
+    return c;
+  }
+};
+// Shared 0..2^14 x B and 0..2^14 x 2^130 B tables in global memory (2 x 2 MiB,
+// L2/MALL-resident), read as 16-byte vectors: too large for LDS, and each lane
+// touches one 128-byte entry of each every third window.
+struct GlobalBTab {
+  const int32_t* w;
+  __device__ __forceinline__ ge_precomp entry(int tb, int j) const {
+    const int4* p = reinterpret_cast<const int4*>(w + (tb * kBEntries + j) * kBStride);
+    int32_t t[32];
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+      const int4 v = p[i];
+      t[4 * i] = v.x; t[4 * i + 1] = v.y; t[4 * i + 2] = v.z; t[4 * i + 3] = v.w;
+    }
+    // words 28, 29 only: loading the two pad words as well let the register
+    // allocator reuse their VGPRs as temporaries, which forced a vmcnt wait
+    // on the whole entry before the window's doublings (the opaque offset
+    // keeps LLVM from widening this 8-byte load back to 16 bytes)
+    const int2 v = *reinterpret_cast<const int2*>(w + (tb * kBEntries + j) * kBStride + opaque_i32(28));
+    t[28] = v.x; t[29] = v.y;
+    return precomp_from_words(t);
+  }
+};
+
+__device__ __forceinline__ void load_words(uint32_t* out, const uint32_t* p, int n4) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int k = 0; k < n4; k++) {
+    const uint4 v = q[k];
+    out[4 * k] = v.x; out[4 * k + 1] = v.y; out[4 * k + 2] = v.z; out[4 * k + 3] = v.w;
+  }
+}
+
+// Launches edv_prep_kernel (edv_prep.hip) over `grid` workgroups on stream s.
+hipError_t launch_prep_kernel(unsigned grid, hipStream_t s, const VerifyArgs& va);
+
+}  // namespace edv

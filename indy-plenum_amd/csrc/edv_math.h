@@ -155,7 +155,7 @@ EDV_HD fe fe_carry64_biased(int64_t h0, int64_t h1, int64_t h2, int64_t h3, int6
 // interleaving buys little ILP but multiplies live registers (measured: a point
 // addition went from 421 to 135 VGPRs), and occupancy is what hides latency here.
 EDV_HD void sched_fence() {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(EDV_NO_SCHED_FENCE)
   __builtin_amdgcn_sched_barrier(0);
 #endif
 }

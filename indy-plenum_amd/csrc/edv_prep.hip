@@ -1,0 +1,79 @@
+// edv_prep.hip -- the prep kernel (phase 1 of a chunk: SURVEY.md section 8a
+// rows V2-V7 plus the half-size scalars and the per-signature point tables),
+// in its own translation unit so it is compiled without the field
+// arithmetic's scheduling fences (see edv_kernels.h).
+#define EDV_NO_SCHED_FENCE 1
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "edv_kernels.h"
+
+namespace edv {
+namespace {
+
+// Phase 1 in three independent sides, interleaved by workgroup (block b runs
+// side b % 3 of slots [(b / 3) 256, +256)): 0 = V2-V4 checks, V6/V7 hash,
+// half-size scalars and digits; 1 = decompress A, 0..16 x (-A) table; 2 = the
+// same for R.  They share no data, so they run side by side (three waves per
+// SIMD at 64k signatures where one kernel per side would leave one wave each
+// to hide its own latencies), and the two exponentiations no longer sit
+// behind the hash in one lane.
+__device__ __forceinline__ void prep_point_side(const VerifyArgs& a, uint64_t j, int side) {
+  if (j >= a.n) return;
+  const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
+  uint32_t P[8];
+  if (side == 1) load_words(P, a.pks + 8 * i, 2);
+  else load_words(P, a.sigs + 16 * i, 2);
+  GlobalATab tab{(side == 1 ? a.st.atab : a.st.rtab) + j * kAWords};
+  const bool ok = prep_point(P, tab);
+  a.st.alive[side * a.st.cap + j] = ok ? 1 : 0;
+  if (!ok) a.accept[i] = 0;
+}
+#ifndef EDV_PREP_WAVES
+#define EDV_PREP_WAVES 3  // minimum waves per SIMD the prep kernel's register budget must allow (three sides)
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EDV_PREP_WAVES, 8))) void edv_prep_kernel(
+    VerifyArgs a) {
+  const int side = int(blockIdx.x % 3);
+  const uint64_t j = uint64_t(blockIdx.x / 3) * kBlock + threadIdx.x;  // slot within the chunk
+#ifdef EDV_AB_SIDES  // measurement-only variant (wrong verdicts): bit k set = run side k
+  if (!((EDV_AB_SIDES >> side) & 1)) return;
+#endif
+  if (side != 0) {
+    prep_point_side(a, j, side);
+    return;
+  }
+  if (j >= a.n) return;
+  const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
+  uint32_t R[8], S[8], A[8];
+  load_words(R, a.sigs + 16 * i, 2);
+  load_words(S, a.sigs + 16 * i + 8, 2);
+  load_words(A, a.pks + 8 * i, 2);
+  const uint64_t o0 = a.off[i] - a.msg_base, o1 = a.off[i + 1] - a.msg_base;
+  PrepDigits pd;
+  const bool ok = prep_one(R, S, A, a.msgs + o0, o1 - o0, pd);
+  a.st.alive[j] = ok ? 1 : 0;
+  if (ok) {
+    uint32_t* d = a.st.dig + j;
+    const uint64_t cap = a.st.cap;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      d[uint64_t(k) * cap] = pd.da[k];
+      d[uint64_t(8 + k) * cap] = pd.db[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kBDigits; k++) d[uint64_t(kDigB + k) * cap] = pd.bw[k];
+    d[uint64_t(kDigNwin) * cap] = uint32_t(pd.nwin) | (pd.negR ? 0x100u : 0u);
+  } else {
+    a.accept[i] = 0;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_prep_kernel(unsigned grid, hipStream_t s, const VerifyArgs& va) {
+  edv_prep_kernel<<<dim3(grid), dim3(kBlock), 0, s>>>(va);
+  return hipGetLastError();
+}
+
+}  // namespace edv

@@ -26,6 +26,7 @@
 #include <string>
 
 #include "edv_verify_core.h"
+#include "edv_kernels.h"
 #include "edv_sha256.h"
 #include "../../include/edv.h"
 
@@ -33,101 +34,7 @@ using namespace edv;
 
 namespace {
 
-constexpr int kBlock = 256;
-constexpr int kAWords = kAEntries * 40;   // cached point = 4 x 10 limbs (680 words = 2,720 B)
-// dig words per signature: da (8), db (8), B digit pairs (9), window count (1)
-constexpr int kDigWords = 8 + 8 + kBDigits + 1;
-constexpr int kDigB = 16, kDigNwin = 16 + kBDigits;
-constexpr uint64_t kChunkDefault = uint64_t(1) << 18;  // signatures per prep/main launch pair
-
-// Per-chunk state handed from the prep kernel to the main kernel, SoA so every
-// wave-wide load/store touches 64 consecutive words:
-//   atab[680 * i + w]  word w (0..679) of signature i's 0..16 x (-A) table
-//   rtab[680 * i + w]  the same for its 0..16 x (-+R) table
-//   dig[w * cap + i]   w 0..7: packed radix-32 digits of a, 8..15: of |b|,
-//                      16..24: B-scalar digit pairs, 25: windows needed
-//   alive[k cap + i]   1 if prep side k (0 hash, 1 A, 2 R) passed for slot i (the
-//                      main kernel skips lanes where any side failed)
-struct ChunkState {
-  int32_t* atab;
-  int32_t* rtab;
-  uint32_t* dig;
-  uint8_t* alive;
-  uint64_t cap;
-  const uint32_t* perm;   // slot j -> request base + perm[j] (length buckets); null = identity
-};
-
-struct VerifyArgs {
-  const uint32_t* sigs;   // n x 16 words
-  const uint32_t* pks;    // n x 8 words
-  const uint8_t* msgs;
-  const uint64_t* off;    // n + 1
-  uint64_t msg_base;
-  uint64_t base;          // first signature of this chunk
-  uint64_t n;             // signatures in this chunk
-  uint8_t* accept;        // indexed by global signature index
-  ChunkState st;
-  const int32_t* btab;    // kBTables x kBEntries x kBStride
-};
-
 // ---------------------------------------------------------------- kernels
-// Per-signature A table in HBM, signature-major: signature i's 360 words are
-// contiguous at slot = atab + 360*i, so a lane's digit-dependent gather reads
-// 160 contiguous bytes (10 x 16-byte loads) instead of touching one line per
-// word for every distinct digit in the wave (the word-major layout measured
-// 39 KB of L2-miss traffic per verify, 8x the useful bytes).
-struct GlobalATab {
-  int32_t* slot;
-  // one entry = 40 contiguous words (160 B, 16-byte aligned): ten 16-byte stores
-  __device__ __forceinline__ void store(int e, const ge_cached& c) const {
-    int32_t t[40];
-#pragma unroll
-    for (int l = 0; l < 10; l++) {
-      t[l] = c.YpX.v[l]; t[10 + l] = c.YmX.v[l]; t[20 + l] = c.Z.v[l]; t[30 + l] = c.T2d.v[l];
-    }
-    int4* p = reinterpret_cast<int4*>(slot + e * 40);
-#pragma unroll
-    for (int q = 0; q < 10; q++) p[q] = make_int4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
-  }
-  __device__ __forceinline__ ge_cached load(int e) const {
-    const int4* p = reinterpret_cast<const int4*>(slot + e * 40);
-    int32_t t[40];
-#pragma unroll
-    for (int q = 0; q < 10; q++) {
-      const int4 v = p[q];
-      t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
-    }
-    ge_cached c;
-#pragma unroll
-    for (int l = 0; l < 10; l++) {
-      c.YpX.v[l] = t[l]; c.YmX.v[l] = t[10 + l]; c.Z.v[l] = t[20 + l]; c.T2d.v[l] = t[30 + l];
-    }
-    return c;
-  }
-};
-// Shared 0..2^14 x B and 0..2^14 x 2^130 B tables in global memory (2 x 2 MiB,
-// L2/MALL-resident), read as 16-byte vectors: too large for LDS, and each lane
-// touches one 128-byte entry of each every third window.
-struct GlobalBTab {
-  const int32_t* w;
-  __device__ __forceinline__ ge_precomp entry(int tb, int j) const {
-    const int4* p = reinterpret_cast<const int4*>(w + (tb * kBEntries + j) * kBStride);
-    int32_t t[32];
-#pragma unroll
-    for (int i = 0; i < 7; i++) {
-      const int4 v = p[i];
-      t[4 * i] = v.x; t[4 * i + 1] = v.y; t[4 * i + 2] = v.z; t[4 * i + 3] = v.w;
-    }
-    // words 28, 29 only: loading the two pad words as well let the register
-    // allocator reuse their VGPRs as temporaries, which forced a vmcnt wait
-    // on the whole entry before the window's doublings (the opaque offset
-    // keeps LLVM from widening this 8-byte load back to 16 bytes)
-    const int2 v = *reinterpret_cast<const int2*>(w + (tb * kBEntries + j) * kBStride + opaque_i32(28));
-    t[28] = v.x; t[29] = v.y;
-    return precomp_from_words(t);
-  }
-};
-
 // The main kernel's views of the tables: stage() copies the entry a lane needs
 // this window from global memory straight into the wave's LDS slice
 // (global_load_lds_dwordx4: 64 lanes x 16 B per instruction, lane-linear), so
@@ -187,74 +94,14 @@ struct LdsBTab {
   }
 };
 
-__device__ __forceinline__ void load_words(uint32_t* out, const uint32_t* p, int n4) {
-  const uint4* q = reinterpret_cast<const uint4*>(p);
-#pragma unroll
-  for (int k = 0; k < n4; k++) {
-    const uint4 v = q[k];
-    out[4 * k] = v.x; out[4 * k + 1] = v.y; out[4 * k + 2] = v.z; out[4 * k + 3] = v.w;
-  }
-}
-
-// Phase 1 in three independent sides, interleaved by workgroup (block b runs
-// side b % 3 of slots [(b / 3) 256, +256)): 0 = V2-V4 checks, V6/V7 hash,
-// half-size scalars and digits; 1 = decompress A, 0..16 x (-A) table; 2 = the
-// same for R.  They share no data, so they run side by side (three waves per
-// SIMD at 64k signatures where one kernel per side would leave one wave each
-// to hide its own latencies), and the two exponentiations no longer sit
-// behind the hash in one lane.
-__device__ __forceinline__ void prep_point_side(const VerifyArgs& a, uint64_t j, int side) {
-  if (j >= a.n) return;
-  const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
-  uint32_t P[8];
-  if (side == 1) load_words(P, a.pks + 8 * i, 2);
-  else load_words(P, a.sigs + 16 * i, 2);
-  GlobalATab tab{(side == 1 ? a.st.atab : a.st.rtab) + j * kAWords};
-  const bool ok = prep_point(P, tab);
-  a.st.alive[side * a.st.cap + j] = ok ? 1 : 0;
-  if (!ok) a.accept[i] = 0;
-}
-#ifndef EDV_PREP_WAVES
-#define EDV_PREP_WAVES 3  // minimum waves per SIMD the prep kernel's register budget must allow (three sides)
-#endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EDV_PREP_WAVES, 8))) void edv_prep_kernel(
-    VerifyArgs a) {
-  const int side = int(blockIdx.x % 3);
-  const uint64_t j = uint64_t(blockIdx.x / 3) * kBlock + threadIdx.x;  // slot within the chunk
-  if (side != 0) {
-    prep_point_side(a, j, side);
-    return;
-  }
-  if (j >= a.n) return;
-  const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
-  uint32_t R[8], S[8], A[8];
-  load_words(R, a.sigs + 16 * i, 2);
-  load_words(S, a.sigs + 16 * i + 8, 2);
-  load_words(A, a.pks + 8 * i, 2);
-  const uint64_t o0 = a.off[i] - a.msg_base, o1 = a.off[i + 1] - a.msg_base;
-  PrepDigits pd;
-  const bool ok = prep_one(R, S, A, a.msgs + o0, o1 - o0, pd);
-  a.st.alive[j] = ok ? 1 : 0;
-  if (ok) {
-    uint32_t* d = a.st.dig + j;
-    const uint64_t cap = a.st.cap;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      d[uint64_t(k) * cap] = pd.da[k];
-      d[uint64_t(8 + k) * cap] = pd.db[k];
-    }
-#pragma unroll
-    for (int k = 0; k < kBDigits; k++) d[uint64_t(kDigB + k) * cap] = pd.bw[k];
-    d[uint64_t(kDigNwin) * cap] = uint32_t(pd.nwin) | (pd.negR ? 0x100u : 0u);
-  } else {
-    a.accept[i] = 0;
-  }
-}
 
 // Phase 2: V8 multi-scalar walk and the identity check.  The window count is
 // the wave's maximum over its live lanes, so the loop stays wave-uniform.
 __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   __shared__ int32_t lds_main[(kBlock / 64) * kLdsWaveWords];
+#ifdef EDV_AB_SIDES  // prep-only measurement variant: the prep state is incomplete, so do nothing here
+  return;
+#endif
   const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
   const bool live = j < a.n && a.st.alive[j] && a.st.alive[a.st.cap + j] && a.st.alive[2 * a.st.cap + j];
   const uint32_t* d = a.st.dig + j;
@@ -640,8 +487,7 @@ int launch_prep(uint32_t* ctr, const VerifyArgs& va, const uint64_t* d_off, bool
                                                                      const_cast<uint32_t*>(va.st.perm));
     HIPOK(hipGetLastError(), "bucket launch");
   }
-  edv_prep_kernel<<<dim3(3 * blocks), dim3(kBlock), 0, s>>>(va);  // hash, A and R sides
-  HIPOK(hipGetLastError(), "prep launch");
+  HIPOK(launch_prep_kernel(3 * blocks, s, va), "prep launch");  // hash, A and R sides
   return 0;
 }
 int launch_main(const VerifyArgs& va, hipStream_t s) {
@@ -1243,7 +1089,7 @@ int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uin
                                                                                const_cast<uint32_t*>(va.st.perm));
     }
     HIPOK(hipEventRecord(ev.e[0], c->stream), "record");
-    edv_prep_kernel<<<dim3(3 * blocks), dim3(kBlock), 0, c->stream>>>(va);
+    HIPOK(launch_prep_kernel(3 * blocks, c->stream, va), "prep launch");
     HIPOK(hipEventRecord(ev.e[1], c->stream), "record");
     edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(va);
     HIPOK(hipEventRecord(ev.e[2], c->stream), "record");

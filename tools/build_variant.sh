@@ -6,5 +6,5 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p $R/indy-plenum_amd/variants
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -Wall -Wno-unused-function $2 \
-  $R/indy-plenum_amd/csrc/edv_verify.hip -o $R/indy-plenum_amd/variants/libedv_$1.so
+  $R/indy-plenum_amd/csrc/edv_verify.hip $R/indy-plenum_amd/csrc/edv_prep.hip -o $R/indy-plenum_amd/variants/libedv_$1.so
 echo built variants/libedv_$1.so

@@ -35,7 +35,7 @@ N_SIMD = 256 * 4
 
 
 def short(name):
-    return name.replace("(anonymous namespace)::", "").split("(")[0]
+    return name.replace("(anonymous namespace)::", "").split("(")[0].split("::")[-1]
 
 
 def collect(root):
