@@ -789,6 +789,110 @@ fail:
   return nullptr;
 }
 
+// ------------------------------------------------- request digests (f-3)
+// request_digests(reqs, sha_addr, device_mask) -> list of hex str or None
+// Request.getDigest() (plenum/common/request.py:71-72) for each request dict:
+// sha256(serialize_msg_for_signing(signingState())).hexdigest(), signingState =
+// {identifier, reqId, operation[, protocolVersion if not None]}
+// (request.py:77-87).  Those four keys sort as identifier < operation <
+// protocolVersion < reqId, so the serialization is written directly, without
+// building the dict.  All messages go to one edv_sha256_batch call at sha_addr
+// (GIL released).  None: a request this path does not handle (not a dict, no
+// identifier -- the reference derives one from the signatures --, or a value
+// the native serializer leaves to Python); the caller computes those in Python.
+typedef int (*sha_fn_t)(const uint8_t*, const uint64_t*, uint64_t, uint8_t*, uint32_t);
+PyObject *g_k_reqid, *g_k_operation, *g_k_protocol;
+
+PyObject* py_request_digests(PyObject*, PyObject* args) {
+  PyObject* reqs;
+  unsigned long long sha_addr;
+  unsigned int mask;
+  if (!PyArg_ParseTuple(args, "OKI", &reqs, &sha_addr, &mask)) return nullptr;
+  PyObject* seq = PySequence_Fast(reqs, "request_digests needs a sequence");
+  if (!seq) return nullptr;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  std::string msgs;
+  msgs.reserve(size_t(n) * 160);
+  std::vector<uint64_t> off(1, 0);
+  std::vector<Py_ssize_t> where;  // request index of each hashed message
+  where.reserve(size_t(n));
+  for (Py_ssize_t k = 0; k < n; k++) {
+    PyObject* r = PySequence_Fast_GET_ITEM(seq, k);
+    if (!PyDict_Check(r)) continue;
+    PyObject* idr = PyDict_GetItemWithError(r, g_k_identifier);
+    if (!idr) {
+      if (PyErr_Occurred()) { Py_DECREF(seq); return nullptr; }
+      continue;
+    }
+    const int truth = PyObject_IsTrue(idr);
+    if (truth < 0) { Py_DECREF(seq); return nullptr; }
+    if (!truth) continue;
+    PyObject* op = PyDict_GetItemWithError(r, g_k_operation);
+    PyObject* rid = op || !PyErr_Occurred() ? PyDict_GetItemWithError(r, g_k_reqid) : nullptr;
+    PyObject* pv = (op || !PyErr_Occurred()) && (rid || !PyErr_Occurred()) ? PyDict_GetItemWithError(r, g_k_protocol)
+                                                                           : nullptr;
+    if (PyErr_Occurred()) { Py_DECREF(seq); return nullptr; }
+    const size_t mark = msgs.size();
+    int rc = 1;
+    msgs += "identifier:";
+    rc = ser(idr, 1, nullptr, msgs);
+    if (rc == 1) {
+      msgs += "|operation:";
+      if (op) rc = ser(op, 1, nullptr, msgs);
+    }
+    if (rc == 1 && pv && pv != Py_None) {
+      msgs += "|protocolVersion:";
+      rc = ser(pv, 1, nullptr, msgs);
+    }
+    if (rc == 1) {
+      msgs += "|reqId:";
+      if (rid) rc = ser(rid, 1, nullptr, msgs);
+    }
+    if (rc < 0) { Py_DECREF(seq); return nullptr; }
+    if (rc == 0) {  // leave this one to Python
+      msgs.resize(mark);
+      continue;
+    }
+    off.push_back(uint64_t(msgs.size()));
+    where.push_back(k);
+  }
+  const size_t m = where.size();
+  std::vector<uint8_t> dig(32 * m);
+  int rc = 0;
+  if (m) {
+    msgs.append(64, '\0');  // the kernel's tail loads may read past the last message
+    sha_fn_t sha = reinterpret_cast<sha_fn_t>(sha_addr);
+    Py_BEGIN_ALLOW_THREADS
+    rc = sha(reinterpret_cast<const uint8_t*>(msgs.data()), off.data(), uint64_t(m), dig.data(), mask);
+    Py_END_ALLOW_THREADS
+  }
+  Py_DECREF(seq);
+  if (rc != 0) {
+    PyErr_Format(PyExc_RuntimeError, "edv_sha256_batch failed (%d)", rc);
+    return nullptr;
+  }
+  PyObject* out = PyList_New(n);
+  if (!out) return nullptr;
+  for (Py_ssize_t k = 0; k < n; k++) {
+    Py_INCREF(Py_None);
+    PyList_SET_ITEM(out, k, Py_None);
+  }
+  static const char hexd[] = "0123456789abcdef";
+  for (size_t i = 0; i < m; i++) {
+    char h[64];
+    for (int b = 0; b < 32; b++) {
+      h[2 * b] = hexd[dig[32 * i + b] >> 4];
+      h[2 * b + 1] = hexd[dig[32 * i + b] & 15];
+    }
+    PyObject* v = PyUnicode_FromStringAndSize(h, 64);
+    if (!v) { Py_DECREF(out); return nullptr; }
+    PyObject* old = PyList_GET_ITEM(out, where[i]);
+    PyList_SET_ITEM(out, where[i], v);
+    Py_DECREF(old);
+  }
+  return out;
+}
+
 PyMethodDef kMethods[] = {
     {"auth_core_batch", py_auth_core_batch, METH_VARARGS,
      "whole-batch CoreAuthNr fast path with the GPU verify inside: (out, slow, rejected)"},
@@ -799,6 +903,8 @@ PyMethodDef kMethods[] = {
     {"b58decode", py_b58decode, METH_O, "base58 1.0.0 b58decode fast path (NotImplemented = use Python)"},
     {"b58encode", py_b58encode, METH_O, "base58 1.0.0 b58encode fast path (NotImplemented = use Python)"},
     {"serialize", py_serialize, METH_VARARGS, "SigningSerializer.serialize fast path (NotImplemented = use Python)"},
+    {"request_digests", py_request_digests, METH_VARARGS,
+     "Request.getDigest for a batch: one edv_sha256_batch call at sha_addr (None = use Python)"},
     {"pack_open_batch", py_pack_open_batch, METH_O, "pack (sig, msg, pk) items into the edv C-ABI layout"},
     {nullptr, nullptr, 0, nullptr}};
 
@@ -812,6 +918,9 @@ PyMODINIT_FUNC PyInit__edvhost(void) {
   g_k_identifier = PyUnicode_InternFromString("identifier");
   g_k_signature = PyUnicode_InternFromString("signature");
   g_k_verkey = PyUnicode_InternFromString("verkey");
+  g_k_reqid = PyUnicode_InternFromString("reqId");
+  g_k_operation = PyUnicode_InternFromString("operation");
+  g_k_protocol = PyUnicode_InternFromString("protocolVersion");
   if (!g_k_identifier || !g_k_signature || !g_k_verkey) return nullptr;
   return PyModule_Create(&kModule);
 }

@@ -10,7 +10,7 @@ edv_sha256_batch call (gfx950 kernel edv_sha256_kernel) for the whole batch:
   plenum/server/domain_req_handler.py:166-167   nym_to_state_key(nym)
       sha256(nym.encode()).digest()
 """
-from . import edv
+from . import _edvhost, edv
 from .constants import IDENTIFIER, OPERATION, PROTOCOL_VERSION, REQ_ID, SIGNATURES
 from .signing_serializer import serialize_msg_for_signing
 
@@ -31,9 +31,18 @@ def signing_state(req, identifier=None):
 
 
 def request_digests(reqs, device_mask: int = 0):
-    """[Request.getDigest() for each request dict], one GPU batch."""
-    return [d.hex() for d in edv.sha256_batch([serialize_msg_for_signing(signing_state(r)) for r in reqs],
-                                              device_mask)]
+    """[Request.getDigest() for each request dict], one GPU batch.  The usual
+    request (a dict with an identifier) is serialized natively and hashed in the
+    same native call (_edvhost.request_digests, GIL released during the GPU
+    call); the rest takes the Python serializer and a second batch."""
+    reqs = list(reqs)
+    out = _edvhost.request_digests(reqs, edv.sha256_address(), device_mask) if reqs else []
+    rest = [k for k, d in enumerate(out) if d is None]
+    if rest:
+        for k, d in zip(rest, edv.sha256_batch([serialize_msg_for_signing(signing_state(reqs[k])) for k in rest],
+                                               device_mask)):
+            out[k] = d.hex()
+    return out
 
 
 def nym_state_keys(nyms, device_mask: int = 0):

@@ -244,6 +244,7 @@ def open_batch(items, device_mask: int = 0):
 
 _OPEN_BATCH = open_batch        # the genuine entry point (tests may monkeypatch open_batch)
 _verify_addr = None
+_sha_addr = None
 BATCH_DEVICE_MASK = 0          # devices used by the native whole-batch authenticator path
 PREP_THREADS = int(os.environ.get("EDV_PREP_THREADS", "0")) or max(1, min(8, (os.cpu_count() or 2) // 2))
 
@@ -259,6 +260,15 @@ def verify_address() -> int:
                                     ctypes.cast(h.edv_host_free, ctypes.c_void_p).value)
         _verify_addr = ctypes.cast(h.edv_verify_batch, ctypes.c_void_p).value
     return _verify_addr
+
+
+def sha256_address() -> int:
+    """Address of edv_sha256_batch (the native request-digest batch calls it with
+    the GIL released)."""
+    global _sha_addr
+    if _sha_addr is None:
+        _sha_addr = ctypes.cast(lib().edv_sha256_batch, ctypes.c_void_p).value
+    return _sha_addr
 
 
 def native_batch_enabled() -> bool:

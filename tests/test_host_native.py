@@ -263,3 +263,48 @@ def test_whole_batch_native_path_equals_sequential(monkeypatch, threads):
     got_ra = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in got_ra]
     assert got_ra == want_ra
     monkeypatch.setattr(edv, "open_batch", real_open)
+
+
+def test_native_request_digests_equal_request_get_digest(monkeypatch):
+    """_edvhost.request_digests (native signingState serialization + one SHA-256
+    batch call, here the kernel's SHA-256 compiled for the CPU) gives
+    Request.getDigest = sha256(serialize_msg_for_signing(signingState)) for every
+    request it takes, and None (Python path) for the rest; digest.request_digests
+    equals the per-request reference restatement on a mixed batch."""
+    import ctypes
+    import hashlib
+    import hostcheck_lib
+    from indy_plenum_amd import digest
+    hc = hostcheck_lib.load()
+    addr = ctypes.cast(hc.hc_sha256_batch, ctypes.c_void_p).value
+    r = random.Random(41)
+    reqs = []
+    for i in range(400):
+        q = {"identifier": base58.b58encode(bytes(r.randrange(256) for _ in range(16))).decode(),
+             "reqId": r.choice([1539648000000000 + i, None, -5, 2**70, 3.5]),
+             "operation": r.choice([{"type": "1", "dest": "x" * r.randrange(40), "verkey": "~abc"},
+                                    {"type": "101", "data": {"nested": [1, "two", None, True]}}, None, "op"]),
+             "signature": "sig"}
+        pv = r.choice([None, 2, 1, "2", "missing"])
+        if pv != "missing":
+            q["protocolVersion"] = pv
+        if r.random() < 0.05:
+            q.pop("identifier")
+            q["signatures"] = {"B": "s", "A": "t"}   # identifier derived from the signatures: Python path
+        if r.random() < 0.03:
+            q["identifier"] = ""                      # falsy identifier: Python path
+            q["signatures"] = {"C": "s"}
+        reqs.append(q)
+    want = [hashlib.sha256(serialize_msg_for_signing(digest.signing_state(q))).hexdigest() for q in reqs]
+    got = _edvhost.request_digests(reqs, addr, 0)
+    assert len(got) == len(reqs)
+    handled = [k for k, d in enumerate(got) if d is not None]
+    assert len(handled) > 300
+    assert all(got[k] == want[k] for k in handled)
+    assert all(reqs[k].get("identifier") for k in handled)
+
+    def cpu_sha256_batch(messages, device_mask=0):
+        return [hashlib.sha256(m).digest() for m in messages]
+    monkeypatch.setattr(edv, "sha256_address", lambda: addr)
+    monkeypatch.setattr(edv, "sha256_batch", cpu_sha256_batch)
+    assert digest.request_digests(reqs) == want
