@@ -25,11 +25,19 @@ prod's client REQUESTs and PROPAGATEs through ONE authenticate_batch call
 (node_integration.authenticate_prod), `batched=False` is the reference's
 one-message-at-a-time verifySignature.  Request keys are Request.getDigest
 (request.py:71-72) values computed by `digest_fn`.
+
+`overlap=True` (batched only) submits a prod's digest + authentication batch to
+a background thread and handles its verdicts at the node's next prod, so the
+GPU round trip of one node's batch runs while the nodes do their Python work
+(the native batch call releases the GIL for base58 decoding and the device
+call).  Each message is still handled exactly once with its own verdict, in
+arrival order; it is only handled one prod later.
 """
 import hashlib
 import json
 import time
 from collections import deque
+from concurrent.futures import ThreadPoolExecutor
 
 from .node_integration import DEFAULT_LISTENER_QUOTA, authenticate_prod, failed
 from .signing_serializer import serialize_msg_for_signing
@@ -41,6 +49,12 @@ NAMES = ("Alpha", "Beta", "Gamma", "Delta", "Epsilon", "Zeta", "Eta", "Theta")
 def cpu_digests(reqs):
     """Request.getDigest on the host (hashlib), one request at a time."""
     return [hashlib.sha256(serialize_msg_for_signing(signing_state(r))).hexdigest() for r in reqs]
+
+
+def _as_outcome(r):
+    """authenticate_batch's per-request result as authenticate_prod's outcome:
+    the identifier set, or the exception instance verifySignature would raise."""
+    return r
 
 
 class _ReqState:
@@ -75,8 +89,11 @@ class _TimedAuth:
 
 class PoolNode:
     def __init__(self, name, peers, authenticator, f, batched=True, digest_fn=cpu_digests,
-                 client_quota=DEFAULT_LISTENER_QUOTA, node_quota=DEFAULT_LISTENER_QUOTA, max_batch=1000):
+                 client_quota=DEFAULT_LISTENER_QUOTA, node_quota=DEFAULT_LISTENER_QUOTA, max_batch=1000,
+                 executor=None):
         self.name, self.peers, self.f = name, list(peers), f
+        self.executor = executor if batched else None  # overlap mode: the pool's background thread
+        self._pending = None          # (future, clients, props) of the previous prod (overlap mode)
         self.auth = _TimedAuth(authenticator, self)
         self.n = len(self.peers) + 1
         self.batched, self.digest_fn = batched, digest_fn
@@ -127,7 +144,18 @@ class PoolNode:
                 (props if m["op"] == "PROPAGATE" else three_pc).append((m, frm))
         clients = [(json.loads(self.client_inbox.popleft()), "client")
                    for _ in range(min(self.client_quota, len(self.client_inbox)))]
-        if props or clients:
+        if self.executor is not None:
+            pend, self._pending = self._pending, None
+            if props or clients:
+                self.verifies += len(props) + len(clients)
+                self.auth_calls += 1
+                reqs = [m["request"] for m, _ in props] + [m for m, _ in clients]
+                ta = time.perf_counter()
+                self._pending = (self.executor.submit(self._digest_and_auth, reqs), clients, props)
+                self.auth_s += time.perf_counter() - ta
+            if pend is not None:
+                self._finish(*pend)
+        elif props or clients:
             ta = time.perf_counter()
             keys = self.digest_fn([m["request"] for m, _ in props] + [m for m, _ in clients])
             self.auth_s += time.perf_counter() - ta
@@ -135,12 +163,29 @@ class PoolNode:
             self.verifies += len(props) + len(clients)
             self.auth_calls += 1 if self.batched else len(props) + len(clients)
             authenticate_prod(self.auth, clients, props, self._on_client, self._on_propagate, self.batched)
+        n_work = len(props) + len(clients) + len(three_pc) + (self._pending is not None)
         for m, frm in three_pc:
             getattr(self, "_on_" + m["op"])(m, frm)
         self._service_replica()
         self.flush(pool)
         self.busy_s += time.perf_counter() - t0
-        return len(props) + len(clients) + len(three_pc)
+        return n_work
+
+    # overlap mode: one prod's digests and verdicts, computed in the background
+    def _digest_and_auth(self, reqs):
+        keys = self.digest_fn(reqs)
+        return keys, self.auth._auth.authenticate_batch(reqs)
+
+    def _finish(self, fut, clients, props):
+        ta = time.perf_counter()
+        keys, results = fut.result()      # the node thread waits only for what did not overlap
+        self.auth_s += time.perf_counter() - ta
+        self._keys = iter(keys)
+        it = iter(results)
+        for msg, frm in props:
+            self._on_propagate(msg, frm, _as_outcome(next(it)))
+        for msg, frm in clients:
+            self._on_client(msg, frm, _as_outcome(next(it)))
 
     # ------------------------------------------------------- requests
     def _on_client(self, req, frm, outcome):
@@ -249,11 +294,13 @@ class Pool:
     """n nodes (f = (n - 1) // 3), primary = the first; `auth_factory(name)`
     returns each node's ReqAuthenticator."""
 
-    def __init__(self, auth_factory, n=4, batched=True, digest_fn=cpu_digests, **node_kw):
+    def __init__(self, auth_factory, n=4, batched=True, digest_fn=cpu_digests, overlap=False, **node_kw):
         names = NAMES[:n]
         f = (n - 1) // 3
+        # one background thread: batches of different nodes reach the device one at a time
+        self.executor = ThreadPoolExecutor(max_workers=1) if overlap and batched else None
         self.nodes = {nm: PoolNode(nm, [p for p in names if p != nm], auth_factory(nm), f, batched, digest_fn,
-                                   **node_kw) for nm in names}
+                                   executor=self.executor, **node_kw) for nm in names}
         self.nodes[names[0]].is_primary = True
 
     def submit(self, reqs):
@@ -271,6 +318,8 @@ class Pool:
         while min(nd.ordered for nd in self.nodes.values()) < expect:
             work = sum(nd.prod(self) for nd in self.nodes.values())
             idle = 0 if work else idle + 1
+        if self.executor is not None:
+            self.executor.shutdown(wait=True)
             if idle > max_idle_rounds:
                 raise RuntimeError("pool stalled: ordered %s of %d" % ([nd.ordered for nd in self.nodes.values()],
                                                                       expect))

@@ -47,8 +47,8 @@ def factory(signers):
     return make
 
 
-@pytest.mark.parametrize("batched", [False, True])
-def test_pool_orders_every_valid_request_once(batched, monkeypatch):
+@pytest.mark.parametrize("batched,overlap", [(False, False), (True, False), (True, True)])
+def test_pool_orders_every_valid_request_once(batched, overlap, monkeypatch):
     calls = []
 
     def oracle(items, device_mask=0):
@@ -57,7 +57,8 @@ def test_pool_orders_every_valid_request_once(batched, monkeypatch):
         return H.oracle_open_batch(items)
     monkeypatch.setattr(edv, "open_batch", oracle)
     signers, reqs, valid = flood()
-    pool = Pool(factory(signers), n=4, batched=batched, digest_fn=cpu_digests, client_quota=16, max_batch=7)
+    pool = Pool(factory(signers), n=4, batched=batched, digest_fn=cpu_digests, overlap=overlap, client_quota=16,
+                max_batch=7)
     pool.submit(reqs)
     wall = pool.run(len(valid))
     st = pool.stats(wall, len(valid))

@@ -19,8 +19,9 @@ from indy_plenum_amd.pool import Pool, cpu_digests
 pytestmark = pytest.mark.gpu
 
 
-def _run(signers, reqs, valid, batched, digest_fn):
-    pool = Pool(factory(signers), n=4, batched=batched, digest_fn=digest_fn, client_quota=50, max_batch=40)
+def _run(signers, reqs, valid, batched, digest_fn, overlap=False):
+    pool = Pool(factory(signers), n=4, batched=batched, digest_fn=digest_fn, overlap=overlap, client_quota=50,
+                max_batch=40)
     pool.submit(reqs)
     wall = pool.run(len(valid))
     st = pool.stats(wall, len(valid))
@@ -28,13 +29,14 @@ def _run(signers, reqs, valid, batched, digest_fn):
     return st
 
 
-def test_pool_c5_gpu_batched_equals_reference_flow(monkeypatch):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_pool_c5_gpu_batched_equals_reference_flow(monkeypatch, overlap):
     assert edv.device_count() >= 1
     signers, reqs, valid = flood(n_valid=400, n_bad_sig=40, n_unknown=20, seed=55)
     with monkeypatch.context() as m:
         m.setattr(edv, "open_batch", H.oracle_open_batch)
         ref = _run(signers, reqs, valid, batched=False, digest_fn=cpu_digests)
-    gpu = _run(signers, reqs, valid, batched=True, digest_fn=digest.request_digests)
+    gpu = _run(signers, reqs, valid, batched=True, digest_fn=digest.request_digests, overlap=overlap)
     assert gpu["ordered_per_node"] == ref["ordered_per_node"] == [len(valid)] * 4
     assert gpu["nacks_per_node"] == ref["nacks_per_node"] == [len(reqs) - len(valid)] * 4
     assert gpu["bad_propagates"] == ref["bad_propagates"] == 0

@@ -62,8 +62,9 @@ def factory(clients, cls):
 
 
 def run(mode, clients, reqs):
-    if mode == "gpu_batched":
-        pool = Pool(factory(clients, CoreAuthNr), n=4, batched=True, digest_fn=digest.request_digests)
+    if mode in ("gpu_batched", "gpu_batched_overlap"):
+        pool = Pool(factory(clients, CoreAuthNr), n=4, batched=True, digest_fn=digest.request_digests,
+                    overlap=mode == "gpu_batched_overlap")
     else:
         pool = Pool(factory(clients, sodium_ref.SodiumCoreAuthNr), n=4, batched=False, digest_fn=cpu_digests)
     native = base58._native
@@ -84,11 +85,14 @@ N_CPU = int(os.environ.get("N_CPU", 2000))
 clients, reqs = make_flood(N)
 warm = run("gpu_batched", clients, reqs[:500])
 out = {"metric": "4-node pool ordered requests/s under a client flood (C5)", "n_nodes": 4, "f": 1,
-       "gpu_batched": run("gpu_batched", clients, reqs)}
+       "gpu_batched": run("gpu_batched", clients, reqs),
+       "gpu_batched_overlap": run("gpu_batched_overlap", clients, reqs)}
 if sodium_ref.sodium() is not None:
     out["cpu_reference"] = run("cpu_reference", clients, reqs[:N_CPU])
     out["speedup_one_process"] = (out["gpu_batched"]["ordered_req_per_s_one_process"]
                                   / out["cpu_reference"]["ordered_req_per_s_one_process"])
     out["speedup_parallel_nodes"] = (out["gpu_batched"]["ordered_req_per_s_parallel_nodes"]
                                      / out["cpu_reference"]["ordered_req_per_s_parallel_nodes"])
+    out["speedup_one_process_overlap"] = (out["gpu_batched_overlap"]["ordered_req_per_s_one_process"]
+                                          / out["cpu_reference"]["ordered_req_per_s_one_process"])
 print(json.dumps(out))
