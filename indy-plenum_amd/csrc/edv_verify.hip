@@ -1,19 +1,20 @@
 // edv_verify.hip -- gfx950 batch Ed25519 verification kernel and the C-ABI of
 // include/edv.h.
 //
-// One signature per lane, 256-thread workgroups, grid-stride over the batch.
-// Per lane (libsodium 1.0.18 semantics):
-//   V2-V4  strictness predicates on S, R, A (bytes only)
-//   V5     decompress -A (one sqrt exponentiation)
-//   V6/V7  SHA-512(R || A || M) straight from the caller's message buffer
-//          (arbitrary byte offsets, padding built in registers), h mod L
-//   V8     R' = [h](-A) + [S]B with FIXED windows so all 64 lanes of a wave
-//          stay in lock-step: h in 64 signed 4-bit digits against a per-lane
-//          table 1..8 x (-A) (cached form, in a coalesced global scratch
-//          buffer), S in 16 signed 16-bit digits against a shared
-//          0..2^15 affine table of j*B (4 MiB, global memory, L2/MALL);
-//          252 doublings, 64 + 16 additions
-//   V9     encode R' (one inversion) and compare its 32 bytes with R
+// One signature per lane, 256-thread workgroups; a chunk of signatures is two
+// launches (libsodium 1.0.18 semantics):
+//   edv_prep_kernel (edv_prep.hip), three sides side by side:
+//     hash side  V2-V4 byte predicates, V6/V7 h = SHA-512(R || A || M) mod L
+//                straight from the caller's message buffer, the half-size
+//                scalars (a, b) with a = b h (mod 8L), b odd, and b S mod L,
+//                recoded into fixed signed windows
+//     A / R side decompress -A / -R (one sqrt exponentiation each) and build
+//                the per-signature 0..16 x P tables (cached form, HBM scratch)
+//   edv_main_kernel (below): [b S]B + [a](-A) + [b](-R) == identity by one
+//     joint walk of ~27 five-bit windows (FIXED windows, so all 64 lanes of a
+//     wave stay in lock-step), table entries staged through LDS, B digits
+//     every third window against two shared 0..2^14 tables; no inversion.
+//   DESIGN.md section 2 has the argument that this is libsodium's verdict.
 // No MFMA: this is scalar bignum integer work (v_mad_i64_i32 chains).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -353,6 +354,9 @@ struct DevCtx {
   hipStream_t hs[kQ] = {};
   hipEvent_t hs_staged[kQ] = {};   // pinned slot q may be refilled once its H2D copies are done
   hipEvent_t hs_end[kQ] = {};
+  // split-prep host path (run_shard_split): copies on hcp, part q's prep on hs[q]
+  hipStream_t hcp = nullptr;
+  hipEvent_t part_copied[kQ] = {}, part_prepped[kQ] = {};
   DevBuf sigs, pks, msgs, off, acc;
   PinnedBuf stage[kQ], acc_host;
   // Pipelined submission (edv_verify_batch_dev_pipelined): two state sets, a
@@ -408,7 +412,10 @@ int ctx_init(DevCtx& c) {
     if (!c.hs[q]) HIPOK(hipStreamCreateWithFlags(&c.hs[q], hipStreamNonBlocking), "hipStreamCreate");
     if (!c.hs_staged[q]) HIPOK(hipEventCreateWithFlags(&c.hs_staged[q], hipEventDisableTiming), "event");
     if (!c.hs_end[q]) HIPOK(hipEventCreateWithFlags(&c.hs_end[q], hipEventDisableTiming), "event");
+    if (!c.part_copied[q]) HIPOK(hipEventCreateWithFlags(&c.part_copied[q], hipEventDisableTiming), "event");
+    if (!c.part_prepped[q]) HIPOK(hipEventCreateWithFlags(&c.part_prepped[q], hipEventDisableTiming), "event");
   }
+  if (!c.hcp) HIPOK(hipStreamCreateWithFlags(&c.hcp, hipStreamNonBlocking), "hipStreamCreate");
   if (!c.st_done) HIPOK(hipEventCreateWithFlags(&c.st_done, hipEventDisableTiming), "event");
   if (const char* e = getenv("EDV_CHUNK")) {
     const uint64_t v = strtoull(e, nullptr, 10);
@@ -576,6 +583,7 @@ int drain(DevCtx& c) {
   HIPOK(hipStreamSynchronize(c.stream), "stream sync");
   HIPOK(hipEventSynchronize(c.st_done), "scratch sync");
   for (int q = 0; q < kQ; q++) HIPOK(hipStreamSynchronize(c.hs[q]), "stream sync");
+  if (c.hcp) HIPOK(hipStreamSynchronize(c.hcp), "stream sync");
   if (c.pipe_ready) {
     HIPOK(hipStreamSynchronize(c.sp), "pipeline sync");
     HIPOK(hipStreamSynchronize(c.sm), "pipeline sync");
@@ -636,6 +644,87 @@ void par_copy(const std::vector<Seg>& segs) {
 
 uint64_t sha512_blocks(const uint64_t* off, uint64_t i) { return (64 + (off[i + 1] - off[i]) + 17 + 127) / 128; }
 
+// Parts for the split-prep host path, 0 = not used.  A shard of one chunk
+// whose messages all have the same SHA-512 block count (no length buckets) is
+// copied in up to kQ parts; the prep of part q runs as soon as part q has
+// landed, on its own stream (a prep wave's latency, not the part's size, sets
+// its time, so the parts' preps run side by side), and one main kernel covers
+// the shard once every part is prepped (the main kernel also takes a whole
+// batch's time at any size, one wave per SIMD).  Measured at C2 (64k x 256 B,
+// profiles/r02/e2e_split_s31_s32.jsonl) it is within the box-to-box noise of the
+// one-sub-batch path (pinned 1.28-1.64 ms against 1.33-1.41 ms: the copy, 0.42
+// ms, is short next to the part's prep and the main kernel it still waits
+// for), so it is off unless EDV_HOST_PARTS (2..4) asks for it.
+int split_parts(const DevCtx& c, uint64_t n, bool varied) {
+  if (varied || n > c.chunk) return 0;
+  int p = 1;
+  if (const char* e = getenv("EDV_HOST_PARTS")) {
+    const int v = atoi(e);
+    if (v >= 1 && v <= kQ) p = v;
+  }
+  if (uint64_t(p) * 64 > n) p = 1;
+  return p > 1 ? p : 0;
+}
+
+// The split-prep host path (see split_parts) for requests [lo, hi) of a host
+// batch; device buffers sized by the caller, h_acc receives the verdicts.
+// Caller holds c.mu.
+int run_shard_split(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
+                    uint64_t lo, uint64_t hi, int parts, bool pinned, uint8_t* d_sigs, uint8_t* d_pks,
+                    uint8_t* d_msgs, uint64_t* d_off, uint8_t* d_acc, uint8_t* h_acc) {
+  const uint64_t n = hi - lo, mbase = off[lo];
+  // the scratch's previous users (any stream) finish before any prep writes it;
+  // the copy stream waits too, so a sequence of calls stays in order
+  HIPOK(hipStreamWaitEvent(c.hcp, c.st_done, 0), "wait scratch");
+  PinnedBuf& sl = c.stage[0];
+  uint8_t* p = nullptr;
+  if (!pinned) {
+    HIPOK(hipEventSynchronize(c.hs_staged[0]), "stage wait");  // the slot's previous H2D is done
+    if (sl.ensure(n * 96 + (n + parts) * 8 + (off[hi] - mbase))) return EDV_E_OOM;
+    p = static_cast<uint8_t*>(sl.p);
+  }
+  int err;
+  for (int q = 0; q < parts; q++) {
+    // part q: requests [a, b); its offsets get a private window of cnt + 1 at d_off + (a - lo) + q
+    const uint64_t a = lo + n * q / parts, b = lo + n * (q + 1) / parts, cnt = b - a;
+    const uint64_t mA = off[a], mB = off[b];
+    uint64_t* d_o = d_off + (a - lo) + q;
+    const uint8_t *src_s = sigs + 64 * a, *src_p = pks + 32 * a, *src_m = msgs + mA;
+    const uint8_t* src_o = reinterpret_cast<const uint8_t*>(off + a);
+    if (!pinned) {
+      // stage part q in the pinned slot (a parallel memcpy) while part q-1's H2D runs
+      uint8_t *ps = p + 64 * (a - lo), *pp = p + 64 * n + 32 * (a - lo), *po = p + 96 * n + 8 * ((a - lo) + q),
+              *pm = p + 96 * n + 8 * (n + parts) + (mA - mbase);
+      par_copy({{ps, src_s, 64 * cnt}, {pp, src_p, 32 * cnt}, {po, src_o, 8 * (cnt + 1)}, {pm, src_m, mB - mA}});
+      src_s = ps; src_p = pp; src_o = po; src_m = pm;
+    }
+    HIPOK(hipMemcpyAsync(d_sigs + 64 * (a - lo), src_s, cnt * 64, hipMemcpyHostToDevice, c.hcp), "h2d sigs");
+    HIPOK(hipMemcpyAsync(d_pks + 32 * (a - lo), src_p, cnt * 32, hipMemcpyHostToDevice, c.hcp), "h2d pks");
+    HIPOK(hipMemcpyAsync(d_o, src_o, (cnt + 1) * 8, hipMemcpyHostToDevice, c.hcp), "h2d off");
+    if (mB > mA) HIPOK(hipMemcpyAsync(d_msgs + (mA - mbase), src_m, mB - mA, hipMemcpyHostToDevice, c.hcp), "h2d msgs");
+    HIPOK(hipEventRecord(c.part_copied[q], c.hcp), "record");
+    hipStream_t s = c.hs[q];
+    HIPOK(hipStreamWaitEvent(s, c.part_copied[q], 0), "wait copy");
+    // slots [a - lo, b - lo) of the chunk scratch, so the main kernel sees the shard as one chunk
+    VerifyArgs va = make_args(c, c.st, d_sigs + 64 * (a - lo), d_pks + 32 * (a - lo), d_msgs, d_o, mbase,
+                              d_acc + (a - lo), false, a - lo);
+    va.n = cnt;
+    if ((err = launch_prep(bucket_ctr(c.st, q), va, d_o, false, s))) return err;
+    HIPOK(hipEventRecord(c.part_prepped[q], s), "record");
+  }
+  if (!pinned) HIPOK(hipEventRecord(c.hs_staged[0], c.hcp), "record");
+  hipStream_t s0 = c.hs[0];
+  for (int q = 1; q < parts; q++) HIPOK(hipStreamWaitEvent(s0, c.part_prepped[q], 0), "wait prep");
+  VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, mbase, d_acc, false, 0);
+  va.n = n;
+  if ((err = launch_main(va, s0))) return err;
+  HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, s0), "d2h accept");
+  HIPOK(hipEventRecord(c.st_done, s0), "record scratch");
+  HIPOK(hipStreamWaitEvent(c.stream, c.st_done, 0), "join");
+  HIPOK(hipStreamSynchronize(s0), "stream sync");
+  return 0;
+}
+
 // One shard on one device, host buffers: sub-batches of P requests go round
 // robin over the kQ host-path streams; per sub-batch: H2D copies (straight
 // from the caller's memory when it is pinned, else through this stream's
@@ -682,8 +771,18 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
   uint64_t* d_off = static_cast<uint64_t*>(c.off.p);
   uint8_t* d_acc = static_cast<uint8_t*>(c.acc.p);
   uint8_t* h_acc = acc_pinned ? accept + lo : static_cast<uint8_t*>(c.acc_host.p);
-  for (int q = 0; q < Q; q++) HIPOK(hipStreamWaitEvent(c.hs[q], c.st_done, 0), "wait scratch");
   int err;
+  // One chunk of fixed-length requests: copy in parts, prep each part as it
+  // lands, one main kernel over the whole shard.
+  if (const int parts = split_parts(c, n, varied)) {
+    if (c.off.ensure((n + parts) * 8)) return EDV_E_OOM;
+    if ((err = run_shard_split(c, sigs, pks, msgs, off, lo, hi, parts, pinned, d_sigs, d_pks, d_msgs,
+                               static_cast<uint64_t*>(c.off.p), d_acc, h_acc)))
+      return err;
+    if (!acc_pinned) memcpy(accept + lo, h_acc, n);
+    return 0;
+  }
+  for (int q = 0; q < Q; q++) HIPOK(hipStreamWaitEvent(c.hs[q], c.st_done, 0), "wait scratch");
   for (uint64_t k = 0; k < nsub; k++) {
     const int q = int(k % Q);
     hipStream_t s = c.hs[q];

@@ -117,6 +117,35 @@ def test_host_path_pinned_and_pageable(n):
     pb.free()
 
 
+@pytest.mark.parametrize("n,parts", [(8192 + 5, "2"), (65536, "4"), (65536, "3"), (100003, "2"), (20000, "1")])
+def test_host_split_prep_path(n, parts, monkeypatch):
+    """Fixed-length shards of one chunk with EDV_HOST_PARTS > 1 take the
+    split-prep host path: the batch is copied in parts, each part prepped as it
+    lands (its own stream, its own slice of the scratch), one main kernel over
+    the whole shard.  Pageable and pinned inputs, 15 % invalid spread over the
+    parts; parts = 1 is the ordinary one-sub-batch path, for comparison."""
+    monkeypatch.setenv("EDV_HOST_PARTS", parts)
+    sigs, pks, msgs, off = orc.corpus(0x5B17 + n, 0, n, mode=0, invalid_permille=150)
+    want = checker(sigs, pks, msgs, off)
+    assert 0 < want.sum() < n
+    assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off), want)
+    bufs = [sigs, pks, off.view(np.uint8), msgs]
+    pb = edv.PinnedBuffer(sum(p.nbytes for p in bufs) + 4 * 64 + n)
+    pos, views = 0, []
+    for p in bufs:
+        v = pb.array[pos:pos + p.nbytes]
+        v[:] = p
+        views.append(v)
+        pos += (p.nbytes + 63) // 64 * 64
+    acc = pb.array[pos:pos + n]
+    for _ in range(2):  # back to back: the second call reuses the staging, events and scratch
+        acc[:] = 7
+        edv._check(edv.lib().edv_verify_batch(views[0].ctypes.data, views[1].ctypes.data, views[3].ctypes.data,
+                                              views[2].ctypes.data, n, acc.ctypes.data, 0))
+        assert np.array_equal(acc, want)
+    pb.free()
+
+
 def test_host_path_chunk_seams_with_sub_batches():
     """Small chunks: the host path's sub-batches then span several chunk-sized
     scratch regions per stream (and one stream when the chunk is tiny)."""

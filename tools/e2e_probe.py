@@ -1,6 +1,7 @@
 """Host-path (edv_verify_batch on host buffers) timing breakdown on one GPU:
 raw pinned H2D of the batch bytes, then the verify call from pageable and from
-pinned inputs for EDV_HOST_STREAMS = 1, 2, 4 (sub-batch streams), median of 7."""
+pinned inputs for EDV_HOST_PARTS = 1, 2, 3, 4 (split-prep parts; 1 = one
+sub-batch: copy, prep, main in sequence), median of 7."""
 import json
 import os
 import statistics
@@ -49,8 +50,8 @@ out = {"n": n, "bytes": total,
        "raw_h2d_pageable_ms": med(lambda: d.upload(np.concatenate([p.view(np.uint8) for p in parts])))}
 s = edv.stream(0)
 out["device_resident_ms"] = med(lambda: (b.verify(stream=s), edv.sync(0)))
-for q in (1, 2, 4):
-    os.environ["EDV_HOST_STREAMS"] = str(q)
+for q in (1, 2, 3, 4):
+    os.environ["EDV_HOST_PARTS"] = str(q)
     call(sigs, pks, msgs, off, acc)
     out["pageable_q%d_ms" % q] = med(lambda: call(sigs, pks, msgs, off, acc))
     call(views[0], views[1], views[3], views[2].view(np.uint64), pacc)
