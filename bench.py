@@ -272,8 +272,34 @@ def e2e_leg(batch, device_value, reps=5):
     call(ps, pp, pm, po, pa)
     assert np.array_equal(pa, want)
     t_pin = median_time(lambda: call(ps, pp, pm, po, pa), reps)
+    # back to back through edv_verify_batch_async: batch k+1's copies run while
+    # batch k computes (two verdict arrays in turn, waits one batch behind)
+    pa2 = np.zeros(n, np.uint8)
+    k_async = 10
+
+    def stream_of_batches(s, p, m, o, accs):
+        prev = None
+        for k in range(k_async):
+            t = edv.verify_async(s, p, m, o, accs[k % 2], device=batch.device)
+            if prev is not None:
+                edv.wait_async(prev, device=batch.device)
+            prev = t
+        edv.wait_async(prev, device=batch.device)
+
+    acc2 = np.zeros(n, np.uint8)
+    stream_of_batches(sigs, pks, msgs, off, (acc, acc2))
+    assert np.array_equal(acc, want) and np.array_equal(acc2, want)
+    t_apage = median_time(lambda: stream_of_batches(sigs, pks, msgs, off, (acc, acc2)), reps) / k_async
+    stream_of_batches(ps, pp, pm, po, (pa, pa2))
+    assert np.array_equal(pa, want) and np.array_equal(pa2, want)
+    t_apin = median_time(lambda: stream_of_batches(ps, pp, pm, po, (pa, pa2)), reps) / k_async
     pb.free()
-    return {"what": "edv_verify_batch on host buffers: H2D + kernels + D2H, synchronous, median of %d calls" % reps,
+    return {"what": "edv_verify_batch on host buffers: H2D + kernels + D2H, synchronous, median of %d calls; "
+                    "async_*: %d batches back to back through edv_verify_batch_async (waits one batch behind), "
+                    "median of %d such runs" % (reps, k_async, reps),
+            "async_pinned_verifies_per_s": n / t_apin, "async_pinned_ms_per_batch": 1e3 * t_apin,
+            "async_pageable_verifies_per_s": n / t_apage, "async_pageable_ms_per_batch": 1e3 * t_apage,
+            "async_pinned_vs_device_resident": (n / t_apin) / device_value,
             "requests": n, "pageable_verifies_per_s": n / t_page, "pageable_ms": 1e3 * t_page,
             "pinned_verifies_per_s": n / t_pin, "pinned_ms": 1e3 * t_pin,
             "pinned_vs_device_resident": (n / t_pin) / device_value,

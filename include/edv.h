@@ -22,7 +22,8 @@
  * INTEGRATION.md); every sig here is exactly 64 bytes.
  *
  * All entry points return 0 on success or a negative EDV_E_* code, never
- * throw, and keep no pointer to caller memory after returning.
+ * throw, and keep no pointer to caller memory after returning (except
+ * edv_verify_batch_async, until edv_wait_async for that batch returns).
  */
 #ifndef EDV_H
 #define EDV_H
@@ -41,8 +42,10 @@ extern "C" {
 
 /*
  * Verify n detached signatures held in HOST memory; synchronous.
- * Each device's shard is walked in sub-batches over four streams: H2D copies of
- * one overlap the kernels of the others.  Inputs in pinned memory (e.g. from
+ * A device's shard of up to one chunk (2^18 requests, edv_set_chunk) is one
+ * sub-batch: H2D copies, kernels, D2H of the verdicts; a larger shard alternates
+ * two streams of half-chunk sub-batches, so the copies of one overlap the
+ * kernels of the other.  Inputs in pinned memory (e.g. from
  * edv_host_alloc) are copied to the device directly; pageable inputs are first
  * staged through the library's pinned buffers by a parallel memcpy
  * (EDV_COPY_THREADS threads, default 8).
@@ -60,6 +63,25 @@ extern "C" {
  */
 int edv_verify_batch(const uint8_t *sigs, const uint8_t *pks, const uint8_t *msgs, const uint64_t *msg_off,
                      uint64_t n, uint8_t *accept, uint32_t device_mask);
+
+/*
+ * Asynchronous form of edv_verify_batch on one device (the batched call site of
+ * plenum/server/client_authn.py:92-112 when the Node verifies one batch per prod
+ * and keeps going): queues the H2D copies, the kernels and the D2H of the
+ * verdicts and returns a ticket at once.  Batches alternate between two slots,
+ * so batch k+1's copies (and, for pageable inputs, its staging memcpy, done in
+ * this call) run while batch k computes: back to back, the host path then runs
+ * at the kernels' rate rather than copy + kernels.  The caller's buffers must
+ * stay valid and unchanged, and `accept` unread, until edv_wait_async(device,
+ * ticket) returns 0; a submission waits for the batch two submissions back
+ * (completing it as edv_wait_async would) before reusing its slot.  Same
+ * verdicts, arguments and alignment rules as edv_verify_batch.
+ */
+int edv_verify_batch_async(const uint8_t *sigs, const uint8_t *pks, const uint8_t *msgs, const uint64_t *msg_off,
+                           uint64_t n, uint8_t *accept, int device, int64_t *ticket);
+/* Wait for batch `ticket` of `device` and hand over its verdicts (0 at once if
+ * it already was); EDV_E_ARG for a ticket never issued. */
+int edv_wait_async(int device, int64_t ticket);
 
 /*
  * Same verdicts for inputs already resident in device memory of `device`;
@@ -107,7 +129,9 @@ int edv_sha256_batch_dev(const uint8_t *d_msgs, const uint64_t *d_msg_off, uint6
  * without waiting.  Consecutive submissions alternate between two internal
  * state sets, with the prep kernel (checks, decompression, SHA-512, table) of
  * batch k+1 on one library stream and the main kernel (scalar multiplication,
- * encode) of batch k on another, so both run on the SIMDs at once.  Work
+ * encode) of batch k on another, so both can run on the SIMDs at once
+ * (measured on MI355X at C2 it is slower than sequential batches, 87.6 M
+ * against 90.5 M verifies/s: profiles/r02/ab_pipeline_s30.jsonl).  Work
  * already queued on the library stream (edv_stream) is ordered before the
  * batch; inputs must stay unchanged and each batch's d_accept must not be
  * reused or read until edv_pipeline_sync(device) returns.  Same verdicts as

@@ -357,6 +357,21 @@ struct DevCtx {
   // split-prep host path (run_shard_split): copies on hcp, part q's prep on hs[q]
   hipStream_t hcp = nullptr;
   hipEvent_t part_copied[kQ] = {}, part_prepped[kQ] = {};
+  // asynchronous host path (edv_verify_batch_async): two slots used in turn,
+  // H2D copies on hcp, kernels and the verdicts' D2H on hac, so the copies of
+  // batch k+1 run while batch k computes
+  struct AsyncSlot {
+    DevBuf sigs, pks, msgs, off, acc;
+    PinnedBuf stage, acc_host;
+    hipEvent_t copied = nullptr, done = nullptr;
+    int64_t ticket = -1;         // batch held by the slot, -1 = none
+    uint8_t* accept = nullptr;   // the caller's verdict buffer
+    uint64_t n = 0;
+    bool acc_pinned = false;     // verdicts DMA'd straight into `accept`
+  };
+  AsyncSlot as[2];
+  hipStream_t hac = nullptr;
+  int64_t next_ticket = 0;
   DevBuf sigs, pks, msgs, off, acc;
   PinnedBuf stage[kQ], acc_host;
   // Pipelined submission (edv_verify_batch_dev_pipelined): two state sets, a
@@ -416,6 +431,11 @@ int ctx_init(DevCtx& c) {
     if (!c.part_prepped[q]) HIPOK(hipEventCreateWithFlags(&c.part_prepped[q], hipEventDisableTiming), "event");
   }
   if (!c.hcp) HIPOK(hipStreamCreateWithFlags(&c.hcp, hipStreamNonBlocking), "hipStreamCreate");
+  if (!c.hac) HIPOK(hipStreamCreateWithFlags(&c.hac, hipStreamNonBlocking), "hipStreamCreate");
+  for (auto& s : c.as) {
+    if (!s.copied) HIPOK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming), "event");
+    if (!s.done) HIPOK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "event");
+  }
   if (!c.st_done) HIPOK(hipEventCreateWithFlags(&c.st_done, hipEventDisableTiming), "event");
   if (const char* e = getenv("EDV_CHUNK")) {
     const uint64_t v = strtoull(e, nullptr, 10);
@@ -584,6 +604,7 @@ int drain(DevCtx& c) {
   HIPOK(hipEventSynchronize(c.st_done), "scratch sync");
   for (int q = 0; q < kQ; q++) HIPOK(hipStreamSynchronize(c.hs[q]), "stream sync");
   if (c.hcp) HIPOK(hipStreamSynchronize(c.hcp), "stream sync");
+  if (c.hac) HIPOK(hipStreamSynchronize(c.hac), "stream sync");  // async batches stay pending until edv_wait_async
   if (c.pipe_ready) {
     HIPOK(hipStreamSynchronize(c.sp), "pipeline sync");
     HIPOK(hipStreamSynchronize(c.sm), "pipeline sync");
@@ -872,6 +893,69 @@ int run_digest_shard(DevCtx& c, const uint8_t* msgs, const uint64_t* off, uint64
   return 0;
 }
 
+// Asynchronous host path.  Wait for a slot's batch and hand over its verdicts.
+int async_complete(DevCtx::AsyncSlot& s) {
+  if (s.ticket < 0) return 0;
+  HIPOK(hipEventSynchronize(s.done), "async wait");
+  if (!s.acc_pinned) memcpy(s.accept, s.acc_host.p, s.n);
+  s.ticket = -1;
+  return 0;
+}
+
+// Queue one host batch: H2D copies on hcp (from the caller's memory when it is
+// pinned, else through the slot's pinned staging, filled here while the
+// previous batch computes), then on hac the kernels and the D2H of the
+// verdicts.  A slot is reused two submissions later, after its batch is
+// complete.  Caller holds c.mu.
+int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
+                 uint64_t n, uint8_t* accept, int64_t* ticket) {
+  const int64_t t = c.next_ticket;
+  DevCtx::AsyncSlot& s = c.as[t & 1];
+  int err;
+  if ((err = async_complete(s))) return err;  // the batch of two submissions ago
+  const uint64_t mbase = off[0], mbytes = off[n] - mbase;
+  if (s.sigs.ensure(n * 64) || s.pks.ensure(n * 32) || s.msgs.ensure(mbytes + 64) || s.off.ensure((n + 1) * 8) ||
+      s.acc.ensure(n))
+    return EDV_E_OOM;
+  const bool pinned = is_pinned(sigs) && is_pinned(pks) && is_pinned(off) && (mbytes == 0 || is_pinned(msgs + mbase));
+  s.acc_pinned = is_pinned(accept);
+  if (!s.acc_pinned && s.acc_host.ensure(n)) return EDV_E_OOM;
+  bool varied = false;
+  for (uint64_t i = 1; i < n && !varied; i++) varied = sha512_blocks(off, i) != sha512_blocks(off, 0);
+  const uint8_t *src_s = sigs, *src_p = pks, *src_m = msgs + mbase;
+  const uint8_t* src_o = reinterpret_cast<const uint8_t*>(off);
+  if (!pinned) {
+    if (s.stage.ensure(n * 96 + (n + 1) * 8 + mbytes)) return EDV_E_OOM;
+    uint8_t* p = static_cast<uint8_t*>(s.stage.p);
+    par_copy({{p, sigs, 64 * n}, {p + 64 * n, pks, 32 * n}, {p + 96 * n, src_o, 8 * (n + 1)},
+              {p + 96 * n + 8 * (n + 1), src_m, mbytes}});
+    src_s = p; src_p = p + 64 * n; src_o = p + 96 * n; src_m = p + 96 * n + 8 * (n + 1);
+  }
+  uint8_t* d_sigs = static_cast<uint8_t*>(s.sigs.p);
+  uint8_t* d_pks = static_cast<uint8_t*>(s.pks.p);
+  uint8_t* d_msgs = static_cast<uint8_t*>(s.msgs.p);
+  uint64_t* d_off = static_cast<uint64_t*>(s.off.p);
+  uint8_t* d_acc = static_cast<uint8_t*>(s.acc.p);
+  HIPOK(hipMemcpyAsync(d_sigs, src_s, n * 64, hipMemcpyHostToDevice, c.hcp), "h2d sigs");
+  HIPOK(hipMemcpyAsync(d_pks, src_p, n * 32, hipMemcpyHostToDevice, c.hcp), "h2d pks");
+  HIPOK(hipMemcpyAsync(d_off, src_o, (n + 1) * 8, hipMemcpyHostToDevice, c.hcp), "h2d off");
+  if (mbytes) HIPOK(hipMemcpyAsync(d_msgs, src_m, mbytes, hipMemcpyHostToDevice, c.hcp), "h2d msgs");
+  HIPOK(hipEventRecord(s.copied, c.hcp), "record");
+  HIPOK(hipStreamWaitEvent(c.hac, s.copied, 0), "wait copy");
+  if ((err = launch(c, d_sigs, d_pks, d_msgs, d_off, mbase, n, d_acc, c.hac,
+                    varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH)))
+    return err;
+  uint8_t* h_acc = s.acc_pinned ? accept : static_cast<uint8_t*>(s.acc_host.p);
+  HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, c.hac), "d2h accept");
+  HIPOK(hipEventRecord(s.done, c.hac), "record");
+  s.ticket = t;
+  s.accept = accept;
+  s.n = n;
+  c.next_ticket = t + 1;
+  *ticket = t;
+  return 0;
+}
+
 // Per-verify cost in SHA-512-block units for the shard split: W(m) of SURVEY.md
 // section 8d is 217,600 + 5,500 * blocks INT32 ops, i.e. ~40 blocks' worth of
 // fixed work (decompress, scalar multiplication, encode) per signature.
@@ -989,6 +1073,33 @@ int edv_verify_batch(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msg
   return for_each_shard(msg_off, n, device_mask, [&](DevCtx& c, uint64_t lo, uint64_t hi) {
     return run_shard(c, sigs, pks, msgs, msg_off, lo, hi, accept);
   });
+}
+
+int edv_verify_batch_async(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* msg_off,
+                           uint64_t n, uint8_t* accept, int device, int64_t* ticket) {
+  g_err.clear();
+  if (!ticket) return set_err(EDV_E_ARG, "null ticket");
+  if (n > 0 && (!sigs || !pks || !msg_off || !accept)) return set_err(EDV_E_ARG, "null pointer");
+  if (n > 0 && !msgs && msg_off[n] != msg_off[0]) return set_err(EDV_E_ARG, "null msgs");
+  int err;
+  if (n > 0 && (err = check_offsets(msg_off, n))) return err;
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  if (n == 0) {
+    *ticket = cl.c->next_ticket++;
+    return 0;
+  }
+  return submit_async(*cl.c, sigs, pks, msgs, msg_off, n, accept, ticket);
+}
+
+int edv_wait_async(int device, int64_t ticket) {
+  g_err.clear();
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  if (ticket < 0 || ticket >= cl.c->next_ticket) return set_err(EDV_E_ARG, "unknown ticket");
+  for (auto& s : cl.c->as)
+    if (s.ticket == ticket) return async_complete(s);
+  return 0;  // already complete (waited for, or its slot was reused)
 }
 
 int edv_sha256_batch(const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, uint8_t* out, uint32_t device_mask) {

@@ -72,6 +72,10 @@ def lib():
         h.edv_verify_batch_dev_flags.restype = ctypes.c_int
         h.edv_verify_batch_dev_pipelined.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_uint32]
         h.edv_verify_batch_dev_pipelined.restype = ctypes.c_int
+        h.edv_verify_batch_async.argtypes = [vp, vp, vp, vp, u64, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+        h.edv_verify_batch_async.restype = ctypes.c_int
+        h.edv_wait_async.argtypes = [ctypes.c_int, ctypes.c_int64]
+        h.edv_wait_async.restype = ctypes.c_int
         h.edv_pipeline_sync.argtypes = [ctypes.c_int]
         h.edv_pipeline_sync.restype = ctypes.c_int
         h.edv_time_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int,
@@ -169,6 +173,31 @@ def verify_arrays(sigs, pks, msgs, offsets, device_mask: int = 0) -> np.ndarray:
     _check(lib().edv_verify_batch(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, off.ctypes.data, n,
                                   accept.ctypes.data, device_mask))
     return accept
+
+
+def verify_async(sigs: np.ndarray, pks: np.ndarray, msgs: np.ndarray, offsets: np.ndarray, accept: np.ndarray,
+                 device: int = 0) -> int:
+    """Queue one host batch (edv_verify_batch_async) and return its ticket.
+
+    The arrays (uint8 sigs/pks/msgs/accept, uint64 offsets, C-ABI layout) must
+    stay alive and unchanged, and `accept` unread, until wait_async(ticket)."""
+    off = offsets
+    n = len(off) - 1
+    if off.dtype != np.uint64 or not off.flags.c_contiguous:
+        raise ValueError("offsets must be a contiguous uint64 array")
+    if sigs.nbytes != 64 * n or pks.nbytes != 32 * n or accept.nbytes < n:
+        raise ValueError("sigs/pks/accept size does not match offsets")
+    if n > 0 and int(off[-1]) > msgs.nbytes:
+        raise ValueError("offsets exceed the message buffer")
+    t = ctypes.c_int64(-1)
+    _check(lib().edv_verify_batch_async(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, off.ctypes.data, n,
+                                        accept.ctypes.data, device, ctypes.byref(t)))
+    return t.value
+
+
+def wait_async(ticket: int, device: int = 0) -> None:
+    """Wait until batch `ticket` has its verdicts in its accept array."""
+    _check(lib().edv_wait_async(device, ticket))
 
 
 def sha256_arrays(msgs, offsets, device_mask: int = 0) -> np.ndarray:

@@ -3,8 +3,8 @@
 * f-4 signer parity: edv_sign_batch_dev == libsodium, byte for byte;
 * scratch ordering across caller streams (two batches in flight on two
   streams at once must each get their own verdicts);
-* the host path: pinned (edv_host_alloc) and pageable inputs, sub-batches over
-  the four host-path streams, chunk seams;
+* the host path: pinned (edv_host_alloc) and pageable inputs, sub-batches,
+  chunk seams, the opt-in split-prep mode and the asynchronous two-slot path;
 * the multi-device path (one host thread per device, edv_shard_split) on
   EDV_VIRTUAL_DEVICES logical devices, against libsodium's committed bitmask
   (C3 split by request index) and the checker (C4 cost-balanced split);
@@ -144,6 +144,62 @@ def test_host_split_prep_path(n, parts, monkeypatch):
                                               views[2].ctypes.data, n, acc.ctypes.data, 0))
         assert np.array_equal(acc, want)
     pb.free()
+
+
+def _pinned_copy(sigs, pks, msgs, off, n):
+    bufs = [sigs, pks, off.view(np.uint8), msgs]
+    pb = edv.PinnedBuffer(sum(p.nbytes for p in bufs) + 5 * 64 + n)
+    pos, views = 0, []
+    for p in bufs:
+        v = pb.array[pos:pos + p.nbytes]
+        v[:] = p
+        views.append(v)
+        pos += (p.nbytes + 63) // 64 * 64
+    return pb, (views[0], views[1], views[3], views[2].view(np.uint64)), pb.array[pos:pos + n]
+
+
+def test_host_async_path():
+    """edv_verify_batch_async / edv_wait_async: batches of fixed and mixed
+    lengths (sizes 20,000 / 4,097 / 65,536 / 1 / 30,000, 15 % invalid) queued
+    back to back from pageable memory, waits one behind, a slot reused without
+    an explicit wait (the submission completes the batch two back), then pinned
+    inputs with pinned verdict buffers in turn; every batch equals the checker."""
+    sizes = (20000, 4097, 65536, 1, 30000)
+    batches = [orc.corpus(0xA5A0 + k, 0, n, mode=k % 2, invalid_permille=150) for k, n in enumerate(sizes)]
+    wants = [checker(*b) for b in batches]
+    accs = [np.full(n, 7, np.uint8) for n in sizes]
+    tickets = []
+    for k, b in enumerate(batches):
+        tickets.append(edv.verify_async(*b, accs[k]))
+        if k == 1:
+            edv.wait_async(tickets[0])
+            assert np.array_equal(accs[0], wants[0])
+    # tickets 1 and 2 were completed by the submissions two after them; waiting is still fine
+    for t in tickets:
+        edv.wait_async(t)
+    for a, w in zip(accs, wants):
+        assert np.array_equal(a, w)
+    with pytest.raises(edv.EdvError):
+        edv.wait_async(tickets[-1] + 100)
+    # pinned inputs and verdicts: DMA straight from and into the caller's memory
+    pinned = [_pinned_copy(*batches[k], sizes[k]) for k in (0, 2)]
+    want2 = [wants[0], wants[2]]
+    for _ in range(2):
+        ts = []
+        for (pb, arrs, acc) in pinned:
+            acc[:] = 7
+            ts.append(edv.verify_async(*arrs, acc))
+        for t in ts:
+            edv.wait_async(t)
+        for (pb, arrs, acc), w in zip(pinned, want2):
+            assert np.array_equal(acc, w)
+    for pb, _a, _c in pinned:
+        pb.free()
+    # the synchronous path in between async batches shares the scratch safely
+    t = edv.verify_async(*batches[4], accs[4])
+    assert np.array_equal(edv.verify_arrays(*batches[2]), wants[2])
+    edv.wait_async(t)
+    assert np.array_equal(accs[4], wants[4])
 
 
 def test_host_path_chunk_seams_with_sub_batches():
