@@ -1089,7 +1089,14 @@ int edv_verify_batch_async(const uint8_t* sigs, const uint8_t* pks, const uint8_
     *ticket = cl.c->next_ticket++;
     return 0;
   }
-  return submit_async(*cl.c, sigs, pks, msgs, msg_off, n, accept, ticket);
+  if ((err = submit_async(*cl.c, sigs, pks, msgs, msg_off, n, accept, ticket))) {
+    // whatever was queued before the failure may still read the caller's
+    // buffers: let it finish before the caller gets the error back
+    (void)hipStreamSynchronize(cl.c->hcp);
+    (void)hipStreamSynchronize(cl.c->hac);
+    (void)hipGetLastError();
+  }
+  return err;
 }
 
 int edv_wait_async(int device, int64_t ticket) {
