@@ -121,7 +121,7 @@ int hc_sha256_batch(const uint8_t* msgs, const uint64_t* off, uint64_t n, uint8_
   return 0;
 }
 void hc_btab(int32_t* out) { memcpy(out, btab().w.data(), sizeof(int32_t) * kBEntries * kBStride); }
-// table t (0: j B, 1: j 2^130 B)
+// table t (0: j B, 1: j 2^kBSplit B)
 int hc_btab_table(int t, int32_t* out) {
   if (t < 0 || t >= kBTables) return -1;
   memcpy(out, btab().w.data() + size_t(t) * kBEntries * kBStride, sizeof(int32_t) * kBEntries * kBStride);
@@ -137,20 +137,26 @@ int hc_half_scalars(const uint8_t* h32, uint8_t* a32, uint8_t* u32) {
   store_words(u32, u, 8);
   return neg ? 1 : 0;
 }
-// B-scalar digit pairs of s (9 words)
+// the walk's layout constants: kAWin, kAEntries, kBBits, kBSplit, kBDigits, kBEvery, kBMinWindows
+void hc_layout(int32_t* out7) {
+  const int32_t v[7] = {kAWin, kAEntries, kBBits, kBSplit, kBDigits, kBEvery, kBMinWindows};
+  memcpy(out7, v, sizeof v);
+}
+// B-scalar digit pairs of s (kBDigits words)
 void hc_recode_bscalar(const uint8_t* s32, uint32_t* out9) {
   uint32_t s[8];
   load_words(s, s32, 8);
   recode_bscalar(out9, s);
 }
 int hc_btab_entries() { return kBEntries; }
-// packed signed digits of a 32-byte scalar: 5 -> recode5 (h, the main loop's windows),
-// 15 -> recode15 (S), 8 -> recode8 (signer), 4 / 16 -> the generic recoder at those radices
+// packed signed digits of a 32-byte scalar at radix 2^bits: 4 (64 digits: the main
+// loop's windows at kAWin = 4), 5 (51 digits), 8 -> recode8 (signer), 15 / 16 -> the
+// generic recoder (17 / 16 digits)
 int hc_recode(const uint8_t* in32, int bits, uint32_t* out8) {
   uint32_t w[8];
   load_words(w, in32, 8);
   if (bits == 4) recode4(out8, w);
-  else if (bits == 5) recode5(out8, w);
+  else if (bits == 5) recode5_fixed(out8, w);
   else if (bits == 8) recode8(out8, w);
   else if (bits == 15) recode15(out8, w);
   else if (bits == 16) recode16(out8, w);

@@ -20,26 +20,38 @@ namespace edv {
 // R' == R (the group has order 8L; a = b h mod 8L, not just mod L, keeps the
 // torsion part of a mixed-order A exact).  R' == R is libsodium's
 // encode(R') == R bytes for canonical, decodable R; any other R is rejected
-// up front, as libsodium's compare would.  ~27 windows of doublings instead of
-// 51, and no inversion at the end; the price is a second decompression (R) and
-// a second per-lane table in the prep kernel.
+// up front, as libsodium's compare would.  ~130 doublings instead of 252, and
+// no inversion at the end; the price is a second decompression (R) and a
+// second per-lane table in the prep kernel.
 //
-// [a](-A), [b](-R): fixed signed windows of 5 bits (digits in [-16, 15], the top
-// one >= 0) against per-lane tables 0..16 x (-A) and 0..16 x (-R); the window
-// count is the wave's maximum over its lanes (26-28 in practice, at most 51).
-// [b S mod L]B = [s_lo]B + [s_hi](2^130 B): 9 signed radix-2^15 digits of each
-// half against shared tables 0..2^14 x B and 0..2^14 x 2^130 B, both added at
-// every third window (15 = 3 x 5 bits) from window 24 down.
-constexpr int kAWin = 5;                        // bits per [a](-A) / [b](-R) window
-constexpr int kAWindows = 51;                   // at most: 51 x 5 = 255 bits >= 253
-constexpr int kAEntries = 17;                   // per-lane table 0..16 x P, cached form (entry 0 = identity)
-constexpr int kBBits = 15;                      // radix 2^15 digits of the B scalar halves
-constexpr int kBSplit = 130;                    // s = s_lo + 2^130 s_hi
-constexpr int kBDigits = 9;                     // digits per half: 9 x 15 = 135 bits >= 130
-constexpr int kBEvery = kBBits / kAWin;         // a B digit every third window
-constexpr int kBMinWindows = kBEvery * (kBDigits - 1) + 1;  // 25: the walk reaches window 24
-constexpr int kBEntries = (1 << (kBBits - 1)) + 1; // per table 0..2^14 x base, affine precomp form (2 MiB)
-constexpr int kBTables = 2;                     // base B and base 2^130 B
+// [a](-A), [b](-R): fixed signed windows of kAWin bits against per-lane tables
+// 0..2^(kAWin-1) x (-A) and x (-R); the window count is the wave's maximum
+// over its lanes.  Default kAWin = 4: digits in [-8, 7] (the top one >= 0),
+// 9-entry tables, 33 windows in practice (34 for a few waves), at most 64.
+// [b S mod L]B = [s_lo]B + [s_hi](2^126 B): 8 signed radix-2^16 digits of each
+// half against shared tables 0..2^15 x B and 0..2^15 x 2^126 B (4 MiB each),
+// both added at every fourth window (16 = 4 x 4 bits) from window 28 down.
+// EDV_AWIN=5 builds the earlier layout for A/B runs: 5-bit windows, 17-entry
+// tables, ~27 windows; radix-2^15 B digits split at 2^130, every third window
+// from window 24.  Measured: 4-bit windows make the prep kernel 17 % faster
+// (half the table) and the main kernel 3 % slower (more additions), net +5 %
+// (profiles/r02/ab_w4_s43.jsonl).
+#ifndef EDV_AWIN
+#define EDV_AWIN 4
+#endif
+static_assert(EDV_AWIN == 4 || EDV_AWIN == 5, "window width 4 or 5");
+constexpr int kAWin = EDV_AWIN;                 // bits per [a](-A) / [b](-R) window
+constexpr int kAWindows = (255 + kAWin - 1) / kAWin;  // at most: 64 x 4 = 256 (51 x 5 = 255) bits >= 253
+constexpr int kAEntries = (1 << (kAWin - 1)) + 1;     // per-lane table 0..8 (0..16) x P, cached form (entry 0 = identity)
+constexpr int kBBits = kAWin == 5 ? 15 : 16;    // radix 2^16 (2^15) digits of the B scalar halves
+constexpr int kBSplit = kAWin == 5 ? 130 : 126; // s = s_lo + 2^126 s_hi (2^130)
+// digits per half: 8 x 16 = 128 bits for s_lo < 2^126 and s_hi < 2^127 (9 x 15 = 135 >= 131); s_hi's top
+// digit may reach 2^15, which 16-bit two's complement cannot hold: main_one reads that one digit unsigned
+constexpr int kBDigits = kAWin == 5 ? 9 : 8;
+constexpr int kBEvery = kBBits / kAWin;         // a B digit every fourth (third) window
+constexpr int kBMinWindows = kBEvery * (kBDigits - 1) + 1;  // 29 (25): the walk reaches window 28 (24)
+constexpr int kBEntries = (1 << (kBBits - 1)) + 1; // per table 0..2^15 (2^14) x base, affine precomp form, 4 (2) MiB
+constexpr int kBTables = 2;                     // base B and base 2^kBSplit B
 static_assert(kBBits % kAWin == 0, "B digits must land on window boundaries");
 constexpr int kCombEntries = 129;               // signer comb rows: 0..128 x 256^i B
 constexpr int kBStride = 32;                    // words per B / comb entry (30 used; 128-byte aligned)
@@ -169,8 +181,9 @@ EDV_HD void recode_signed(uint32_t out[8], const uint32_t s[8]) {
     if (wi + 1 < 8) out[wi + 1] |= uint32_t(pe >> 32);
   }
 }
-// h < L: the 51 radix-32 digits of the [h](-A) windows
+// scalar < 2^253: the kAWindows signed radix-2^kAWin digits of the main loop's windows
 EDV_HD void recode5(uint32_t out[8], const uint32_t h[8]) { recode_signed<kAWin, kAWindows>(out, h); }
+EDV_HD void recode5_fixed(uint32_t out[8], const uint32_t h[8]) { recode_signed<5, 51>(out, h); }
 // h < L: 64 signed radix-16 digits in [-8, 7] (kept for the recoding tests)
 EDV_HD void recode4(uint32_t out[8], const uint32_t h[8]) { recode_signed<4, 64>(out, h); }
 // S (signer scalars): 32 signed radix-256 digits in [-128, 127] (k < 2^253 keeps
@@ -191,18 +204,18 @@ EDV_HD void recode8(uint32_t out[8], const uint32_t s[8]) {
   }
 }
 // 17 signed radix-2^15 digits of a scalar < 2^253 (kept for the recoding tests)
-EDV_HD void recode15(uint32_t out[8], const uint32_t s[8]) { recode_signed<kBBits, 17>(out, s); }
+EDV_HD void recode15(uint32_t out[8], const uint32_t s[8]) { recode_signed<15, 17>(out, s); }
 EDV_HD void recode16(uint32_t out[8], const uint32_t s[8]) { recode_signed<16, 16>(out, s); }
 
-// Number of windows the packed radix-32 digits need: 1 + index of the top
-// nonzero digit (0 for a zero scalar).
+// Number of windows the packed radix-2^kAWin digits need: 1 + index of the
+// top nonzero digit (0 for a zero scalar).
 EDV_HD int digits5_windows(const uint32_t d[8]) {
   int n = 0;
 #pragma unroll
   for (int k = 0; k < kAWindows; k++) {
     const int pos = kAWin * k, wi = pos >> 5, sh = pos & 31;
     const uint64_t win = uint64_t(d[wi]) | (wi + 1 < 8 ? uint64_t(d[wi + 1]) << 32 : 0);
-    n = ((win >> sh) & 31) ? k + 1 : n;
+    n = ((win >> sh) & ((1u << kAWin) - 1)) ? k + 1 : n;
   }
   return n;
 }
@@ -494,9 +507,10 @@ EDV_HD void sc_mul(uint32_t out[8], const uint32_t u[8], const uint32_t s[8]) {
   sc_reduce(out, t);
 }
 
-// B-scalar digits of s < L: word k (k < 9) = radix-2^15 digit k of s_lo = s mod
-// 2^130 in its low 16 bits and digit k of s_hi = s >> 130 in its high 16 bits,
-// both signed (two's complement in 16 bits; |d| <= 2^14, top digits >= 0).
+// B-scalar digits of s < L: word k (k < kBDigits) = radix-2^kBBits digit k of
+// s_lo = s mod 2^kBSplit in its low 16 bits and digit k of s_hi = s >> kBSplit
+// in its high 16 bits, signed (two's complement in 16 bits, |d| <= 2^(kBBits-1),
+// top digits >= 0; s_hi's top digit is read unsigned, see kBDigits).
 EDV_HD void recode_bscalar(uint32_t bw[kBDigits], const uint32_t s[8]) {
   uint32_t lo[8], hi[8];
 #pragma unroll
@@ -514,9 +528,10 @@ EDV_HD void recode_bscalar(uint32_t bw[kBDigits], const uint32_t s[8]) {
     const int pos = kBBits * k, wi = pos >> 5, sh = pos & 31;
     const uint64_t wl = uint64_t(dl[wi]) | (wi + 1 < 8 ? uint64_t(dl[wi + 1]) << 32 : 0);
     const uint64_t wh = uint64_t(dh[wi]) | (wi + 1 < 8 ? uint64_t(dh[wi + 1]) << 32 : 0);
-    // sign-extend the 15-bit fields to 16 bits
-    const uint32_t el = uint32_t(int32_t(uint32_t(wl >> sh) << 17) >> 17) & 0xffffu;
-    const uint32_t eh = uint32_t(int32_t(uint32_t(wh >> sh) << 17) >> 17) & 0xffffu;
+    // sign-extend the kBBits-bit fields to 16 bits (radix 2^16: already 16 bits)
+    constexpr int kX = 32 - kBBits;
+    const uint32_t el = uint32_t(int32_t(uint32_t(wl >> sh) << kX) >> kX) & 0xffffu;
+    const uint32_t eh = uint32_t(int32_t(uint32_t(wh >> sh) << kX) >> kX) & 0xffffu;
     bw[k] = el | (eh << 16);
   }
 }
@@ -545,7 +560,7 @@ EDV_HD ge_p3 base_point(int shift) {
   for (int k = 0; k < shift; k++) B = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(B)));
   return B;
 }
-// j * base for j in [0, 2^14], affine precomp form, written as kBStride words.
+// j * base for j in [0, 2^(kBBits-1)], affine precomp form, written as kBStride words.
 EDV_HD void btab_entry(int32_t* o, int j, const ge_p3& base) {
   const ge_cached Bc = ge_p3_to_cached(base);
   ge_p3 acc = ge_p3_identity();
@@ -564,14 +579,14 @@ EDV_HD void btab_entry(int32_t* o, int j, const ge_p3& base) {
 
 // Per-lane outputs of phase 1 that phase 2 consumes.
 struct PrepDigits {
-  uint32_t da[8];        // packed signed radix-32 digits of a ([a](-A))
-  uint32_t db[8];        // packed signed radix-32 digits of |b| ([b](-R), sign folded into the R table)
+  uint32_t da[8];        // packed signed radix-2^kAWin digits of a ([a](-A))
+  uint32_t db[8];        // packed signed radix-2^kAWin digits of |b| ([b](-R), sign folded into the R table)
   uint32_t bw[kBDigits]; // B-scalar digit pairs (recode_bscalar)
   int nwin;              // windows this lane needs (max over a and |b|)
   bool negR;             // b < 0: the R digits are negated ([b](-R) = [|b|](R))
 };
 
-// 0..16 x P into a per-lane table (entry 0 the identity, so a zero digit needs
+// 0..kAEntries-1 x P into a per-lane table (entry 0 the identity, so a zero digit needs
 // no select).  P comes out of a decompression affine (Z = 1, T = XY), so its
 // cached form doubles as precomp form and each further entry is a mixed
 // addition (3 field products instead of 4).
@@ -630,7 +645,7 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
 }
 
 // Phase 1, point sides (kernel edv_prep_kernel, concurrent with the hash
-// side): decompress -P and build its 0..16 x (-P) table, for P = A (V4, V5:
+// side): decompress -P and build its 0..kAEntries-1 x (-P) table, for P = A (V4, V5:
 // libsodium's checks on the key) and for P = R.  encode(R') is canonical and a
 // curve point's encoding, so R bytes that are non-canonical, of small order
 // (libsodium's blocklist) or decode to no point can never pass: the same three
@@ -644,7 +659,7 @@ EDV_HD bool prep_point(const uint32_t P[8], ATab& tab) {
   return true;
 }
 
-// Phase 2 (kernel edv_main_kernel): Q = [s_lo]B + [s_hi](2^130 B) + [a](-A) +
+// Phase 2 (kernel edv_main_kernel): Q = [s_lo]B + [s_hi](2^kBSplit B) + [a](-A) +
 // [|b|](-+R) by a joint fixed-window walk, top window first -- every lane adds
 // at the same positions, so a wave never diverges -- then Q == identity.
 // nwin: windows to walk (the wave's maximum; >= every lane's own count);
@@ -655,7 +670,9 @@ template <class ATab, class BTab>
 EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int nwin, bool negR, ATab& at, ATab& rt,
                      BTab& bt) {
   nwin = mx(nwin, kBMinWindows);
-  // align window nwin-1 with bits [250, 255)
+  // align window nwin-1 with the top window, bits [kTop, kTop + kAWin)
+  constexpr int kTop = kAWin * (kAWindows - 1);       // 250 (252)
+  constexpr int kTopShl = 32 - kAWin - (kTop - 224);  // 1 (0)
 #pragma unroll 1
   for (int k = nwin; k < kAWindows; k++) {
     shl256<kAWin>(da);
@@ -666,8 +683,8 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
   for (int w = nwin - 1; w >= 0; --w) {
     // stage(...) starts this window's table reads (on the GPU: straight into
     // LDS, no registers held), fetch() picks them up after the doublings
-    const int dA = int32_t(da[7] << 1) >> (32 - kAWin);  // digit at bits [250, 255)
-    const int dR = int32_t(db[7] << 1) >> (32 - kAWin);
+    const int dA = int32_t(da[7] << kTopShl) >> (32 - kAWin);  // digit at bits [kTop, kTop + kAWin)
+    const int dR = int32_t(db[7] << kTopShl) >> (32 - kAWin);
     shl256<kAWin>(da);
     shl256<kAWin>(db);
     at.stage(dA < 0 ? -dA : dA);
@@ -679,7 +696,8 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
 #pragma unroll
       for (int k = kBDigits - 1; k > 0; k--) bw[k] = bw[k - 1];
       d0 = int32_t(pair << 16) >> 16;
-      d1 = int32_t(pair) >> 16;
+      // radix 2^16: s_hi's top digit (the first one walked) may be 2^15, kept unsigned
+      d1 = (kBBits == 16 && w == kBMinWindows - 1) ? int32_t(pair >> 16) : int32_t(pair) >> 16;
       bt.stage(0, d0 < 0 ? -d0 : d0);
       bt.stage(1, d1 < 0 ? -d1 : d1);
     }
@@ -687,7 +705,7 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
     if (w == nwin - 1) {
       p3 = ge_p3_identity();
     } else {
-#pragma unroll
+#pragma unroll 1  // a doubling is ~1k instructions: unrolling buys nothing but code size
       for (int d = 0; d < kAWin - 1; d++) acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
       p3 = ge_p1p1_to_p3(ge_p2_dbl(acc));
     }

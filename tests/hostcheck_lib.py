@@ -26,4 +26,12 @@ def load():
         _lib.hc_half_scalars.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p]
         _lib.hc_recode_bscalar.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
         _lib.hc_verify_batch.argtypes = [ctypes.c_char_p] * 3 + [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        _lib.hc_layout.argtypes = [ctypes.c_void_p]
     return _lib
+
+
+def layout():
+    """The walk's layout constants as built (edv_verify_core.h, EDV_AWIN)."""
+    out = (ctypes.c_int32 * 7)()
+    load().hc_layout(out)
+    return dict(zip(("awin", "aentries", "bbits", "bsplit", "bdigits", "bevery", "bminwindows"), list(out)))

@@ -162,10 +162,10 @@ def _digits(packed, bits):
 
 
 def test_scalar_recoding_radix_4_5_8_15_16():
-    """Signed digits the main loop consumes: h (radix 32, digit in [-16, 15], so
-    |d| indexes the 0..16 per-lane table), S (radix 2^15, |d| <= 2^14 so it
-    indexes the 0..2^14 B table), signer scalars (radix 256), and the generic
-    recoder at radix 16 / 2^16; sum d_k * 2^(bits*k) must give back the scalar."""
+    """Signed digits: radix 16 (the main loop's windows, digit in [-8, 7], so |d|
+    indexes the 0..8 per-lane table) and radix 32 (the EDV_AWIN=5 layout),
+    signer scalars (radix 256), the generic recoder at radix 2^15 / 2^16 (B
+    digits); sum d_k * 2^(bits*k) must give back the scalar."""
     hc = hostcheck_lib.load()
     r = random.Random(12)
     out = (ctypes.c_uint32 * 8)()
@@ -183,17 +183,28 @@ def test_scalar_recoding_radix_4_5_8_15_16():
             assert 0 <= d[-1] <= hi, (bits, hex(v))
 
 
+def test_walk_layout_constants():
+    """The default build walks 4-bit windows (9-entry per-lane tables) with
+    radix-2^16 B digits split at 2^126, added every fourth window from window 28."""
+    lay = hostcheck_lib.layout()
+    assert lay == {"awin": 4, "aentries": 9, "bbits": 16, "bsplit": 126, "bdigits": 8, "bevery": 4,
+                   "bminwindows": 29}
+    # both halves of any B scalar s < L fit their digits: s_lo < 2^126, s_hi < 2^127
+    assert lay["bdigits"] * lay["bbits"] >= max(lay["bsplit"], L.bit_length() - lay["bsplit"]) + 1
+
+
 def test_btab_entries_are_multiples_of_B():
-    """The 0..2^14 x B table (affine y+x, y-x, 2dxy limbs) against the oracle's [j]B."""
+    """The 0..2^(bbits-1) x B table (affine y+x, y-x, 2dxy limbs) against the oracle's [j]B."""
     import oracle_lib as orc
     hc = hostcheck_lib.load()
+    lay = hostcheck_lib.layout()
     n = hc.hc_btab_entries()
-    assert n == 2**14 + 1
+    assert n == 2**(lay["bbits"] - 1) + 1
     tab = (ctypes.c_int32 * (n * 32))()
     hc.hc_btab(tab)
     d = (-121665 * pow(121666, P - 2, P)) % P
     r = random.Random(13)
-    for j in [0, 1, 2, 3, 127, 128, 129, 255, 256, 4097, 16383, 16384] + [r.randrange(n) for _ in range(40)]:
+    for j in [0, 1, 2, 3, 127, 128, 129, 255, 256, 4097, 16383, 16384, n - 2, n - 1] + [r.randrange(n) for _ in range(40)]:
         e = list(tab[32 * j: 32 * j + 32])
         ypx, ymx, xy2d = val(e[0:10]) % P, val(e[10:20]) % P, val(e[20:30]) % P
         inv2 = pow(2, P - 2, P)
@@ -203,21 +214,22 @@ def test_btab_entries_are_multiples_of_B():
         assert enc == orc.scalarmult_base(j.to_bytes(32, "little")), j
 
 
-def test_btab_second_table_is_multiples_of_2_130_B():
-    """Table 1 of the B-scalar walk: j x 2^130 B (s = s_lo + 2^130 s_hi), against
-    the oracle's [j 2^130]B."""
+def test_btab_second_table_is_multiples_of_2_bsplit_B():
+    """Table 1 of the B-scalar walk: j x 2^bsplit B (s = s_lo + 2^bsplit s_hi),
+    against the oracle's [j 2^bsplit]B."""
     import oracle_lib as orc
     hc = hostcheck_lib.load()
+    split = hostcheck_lib.layout()["bsplit"]
     n = hc.hc_btab_entries()
     tab = (ctypes.c_int32 * (n * 32))()
     assert hc.hc_btab_table(1, tab) == 0
     inv2 = pow(2, P - 2, P)
-    for j in [0, 1, 2, 3, 255, 8191, 16384]:
+    for j in [0, 1, 2, 3, 255, 8191, 16384, n - 1]:
         e = list(tab[32 * j: 32 * j + 32])
         ypx, ymx = val(e[0:10]) % P, val(e[10:20]) % P
         y, x = (ypx + ymx) * inv2 % P, (ypx - ymx) * inv2 % P
         enc = int.to_bytes(y | ((x & 1) << 255), 32, "little")
-        assert enc == orc.scalarmult_base(((j << 130) % L).to_bytes(32, "little")), j
+        assert enc == orc.scalarmult_base(((j << split) % L).to_bytes(32, "little")), j
 
 
 N8L = 8 * L
@@ -262,19 +274,24 @@ def test_half_scalars_lattice_reduction():
 
 
 def test_recode_bscalar_digit_pairs():
-    """B-scalar digit pairs: s = sum d_lo,k 2^(15k) + 2^130 sum d_hi,k 2^(15k),
-    |d| <= 2^14 (indexes the 0..2^14 tables), top digits >= 0."""
+    """B-scalar digit pairs: s = sum d_lo,k 2^(bbits k) + 2^bsplit sum d_hi,k
+    2^(bbits k), |d| <= 2^(bbits-1) (indexes the 0..2^(bbits-1) tables), top
+    digits >= 0 (s_hi's top one read unsigned, as the main kernel reads it)."""
     hc = hostcheck_lib.load()
+    lay = hostcheck_lib.layout()
+    bb, split, nd = lay["bbits"], lay["bsplit"], lay["bdigits"]
     r = random.Random(22)
-    out = (ctypes.c_uint32 * 9)()
-    vals = [0, 1, L - 1, 2**130 - 1, 2**130, 2**252, 2**129 + 2**128] + [r.randrange(L) for _ in range(3000)]
+    out = (ctypes.c_uint32 * nd)()
+    vals = [0, 1, L - 1, 2**split - 1, 2**split, 2**252, 2**(split - 1) + 2**(split - 2)]
+    vals += [(2**(bb * k) - 1) % L for k in range(1, 16)] + [(2**split - 1) * k % L for k in (1, 3, 7)]
+    vals += [r.randrange(L) for _ in range(3000)]
     for s in vals:
         hc.hc_recode_bscalar(s.to_bytes(32, "little"), out)
         lo = [((w & 0xffff) ^ 0x8000) - 0x8000 for w in out]
-        hi = [((w >> 16) ^ 0x8000) - 0x8000 for w in out]
-        assert all(abs(d) <= 2**14 for d in lo + hi)
+        hi = [((w >> 16) ^ 0x8000) - 0x8000 for w in out[:-1]] + [out[-1] >> 16]
+        assert all(abs(d) <= 2**(bb - 1) for d in lo + hi), hex(s)
         assert lo[-1] >= 0 and hi[-1] >= 0
-        v = sum(d << (15 * k) for k, d in enumerate(lo)) + (sum(d << (15 * k) for k, d in enumerate(hi)) << 130)
+        v = sum(d << (bb * k) for k, d in enumerate(lo)) + (sum(d << (bb * k) for k, d in enumerate(hi)) << split)
         assert v == s, hex(s)
 
 

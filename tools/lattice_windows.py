@@ -3,10 +3,11 @@
 For random h < L: the prep kernel's rule (Euclid on (8L, h) down to the first
 remainder below 2^128, the shorter odd-b neighbour) and,
 for comparison, the best odd-b vector among small combinations of a
-Lagrange-reduced basis.  Prints, per rule, how many lanes need 25..28 five-bit
-signed windows and how many 64-lane waves do (the main kernel walks each
-wave's maximum).  Used to check that no choice of (a, b) shortens the walk:
-  python tools/lattice_windows.py [lanes]
+Lagrange-reduced basis.  Prints, per rule, how many lanes need each number of
+signed windows of WIDTH bits (default 4, the kernel's kAWin; 5 for the earlier
+layout) and how many 64-lane waves do (the main kernel walks each wave's
+maximum).  Used to check that no choice of (a, b) shortens the walk:
+  python tools/lattice_windows.py [lanes] [width]
 """
 import collections
 import random
@@ -16,13 +17,17 @@ L = 2**252 + 27742317777372353535851937790883648493
 M = 8 * L
 
 
+WIDTH = 4
+
+
 def windows(v):
-    """Windows the recode_signed<5, 51> digits of v need (1 + top nonzero digit)."""
+    """Windows the recode_signed<WIDTH, ...> digits of v need (1 + top nonzero digit)."""
+    nd = (255 + WIDTH - 1) // WIDTH
     carry, top = 0, 0
-    for k in range(51):
-        e = ((v >> (5 * k)) & 31) + carry
-        carry = 0 if k == 50 else (e + 16) >> 5
-        e -= carry * 32
+    for k in range(nd):
+        e = ((v >> (WIDTH * k)) & ((1 << WIDTH) - 1)) + carry
+        carry = 0 if k == nd - 1 else (e + (1 << (WIDTH - 1))) >> WIDTH
+        e -= carry << WIDTH
         if e:
             top = k + 1
     return top
@@ -74,7 +79,9 @@ def best_rule(h, span=6):
 
 
 def main():
+    global WIDTH
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 64 * 1024
+    WIDTH = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     rng = random.Random(1)
     hs = [rng.randrange(L) for _ in range(n)]
     for rule in (kernel_rule, best_rule):
