@@ -15,18 +15,18 @@
 namespace edv {
 
 constexpr int kBlock = 256;
-constexpr int kAWords = kAEntries * 40;   // cached point = 4 x 10 limbs (680 words = 2,720 B)
-// dig words per signature: da (8), db (8), B digit pairs (9), window count (1)
+constexpr int kAWords = kAEntries * 40;   // cached point = 4 x 10 limbs (9 entries: 360 words = 1,440 B)
+// dig words per signature: da (8), db (8), B digit pairs (kBDigits), window count (1)
 constexpr int kDigWords = 8 + 8 + kBDigits + 1;
 constexpr int kDigB = 16, kDigNwin = 16 + kBDigits;
 constexpr uint64_t kChunkDefault = uint64_t(1) << 18;  // signatures per prep/main launch pair
 
 // Per-chunk state handed from the prep kernel to the main kernel, SoA so every
 // wave-wide load/store touches 64 consecutive words:
-//   atab[680 * i + w]  word w (0..679) of signature i's 0..16 x (-A) table
-//   rtab[680 * i + w]  the same for its 0..16 x (-+R) table
-//   dig[w * cap + i]   w 0..7: packed radix-32 digits of a, 8..15: of |b|,
-//                      16..24: B-scalar digit pairs, 25: windows needed
+//   atab[kAWords * i + w]  word w of signature i's 0..kAEntries-1 x (-A) table
+//   rtab[kAWords * i + w]  the same for its 0..kAEntries-1 x (-+R) table
+//   dig[w * cap + i]   w 0..7: packed radix-2^kAWin digits of a, 8..15: of |b|,
+//                      16..: kBDigits B-scalar digit pairs, last: windows needed
 //   alive[k cap + i]   1 if prep side k (0 hash, 1 A, 2 R) passed for slot i (the
 //                      main kernel skips lanes where any side failed)
 struct ChunkState {
@@ -85,9 +85,9 @@ struct GlobalATab {
     return c;
   }
 };
-// Shared 0..2^14 x B and 0..2^14 x 2^130 B tables in global memory (2 x 2 MiB,
+// Shared 0..2^15 x B and 0..2^15 x 2^126 B tables in global memory (2 x 4 MiB,
 // L2/MALL-resident), read as 16-byte vectors: too large for LDS, and each lane
-// touches one 128-byte entry of each every third window.
+// touches one 128-byte entry of each every fourth window.
 struct GlobalBTab {
   const int32_t* w;
   __device__ __forceinline__ ge_precomp entry(int tb, int j) const {

@@ -13,7 +13,7 @@ namespace {
 
 // Phase 1 in three independent sides, interleaved by workgroup (block b runs
 // side b % 3 of slots [(b / 3) 256, +256)): 0 = V2-V4 checks, V6/V7 hash,
-// half-size scalars and digits; 1 = decompress A, 0..16 x (-A) table; 2 = the
+// half-size scalars and digits; 1 = decompress A, 0..8 x (-A) table; 2 = the
 // same for R.  They share no data, so they run side by side (three waves per
 // SIMD at 64k signatures where one kernel per side would leave one wave each
 // to hide its own latencies), and the two exponentiations no longer sit

@@ -9,11 +9,11 @@
 //                scalars (a, b) with a = b h (mod 8L), b odd, and b S mod L,
 //                recoded into fixed signed windows
 //     A / R side decompress -A / -R (one sqrt exponentiation each) and build
-//                the per-signature 0..16 x P tables (cached form, HBM scratch)
+//                the per-signature 0..8 x P tables (cached form, HBM scratch)
 //   edv_main_kernel (below): [b S]B + [a](-A) + [b](-R) == identity by one
-//     joint walk of ~27 five-bit windows (FIXED windows, so all 64 lanes of a
+//     joint walk of ~33 four-bit windows (FIXED windows, so all 64 lanes of a
 //     wave stay in lock-step), table entries staged through LDS, B digits
-//     every third window against two shared 0..2^14 tables; no inversion.
+//     every fourth window against two shared 0..2^15 tables; no inversion.
 //   DESIGN.md section 2 has the argument that this is libsodium's verdict.
 // No MFMA: this is scalar bignum integer work (v_mad_i64_i32 chains).
 #include <hip/hip_runtime.h>
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void edv_bucket_scatter_kernel(const uint64
   if (j < n) perm[wbase[b] + rank] = uint32_t(j);
 }
 
-// j * B and j * 2^130 B for j = 0..2^14 in affine precomp form, once per device
+// j * B and j * 2^kBSplit B for j = 0..2^(kBBits-1) in affine precomp form, once per device
 __global__ void edv_btab_kernel(int32_t* out) {
   const int t = threadIdx.x + blockIdx.x * blockDim.x;
   if (t < kBTables * kBEntries) btab_entry(out + t * kBStride, t % kBEntries, base_point((t / kBEntries) * kBSplit));
