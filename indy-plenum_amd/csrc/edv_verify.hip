@@ -1104,8 +1104,17 @@ int edv_wait_async(int device, int64_t ticket) {
   CtxLock cl(device);
   if (cl.err) return cl.err;
   if (ticket < 0 || ticket >= cl.c->next_ticket) return set_err(EDV_E_ARG, "unknown ticket");
-  for (auto& s : cl.c->as)
-    if (s.ticket == ticket) return async_complete(s);
+  for (auto& s : cl.c->as) {
+    if (s.ticket != ticket) continue;
+    // wait without holding the device lock (other threads keep submitting);
+    // a submission that reuses the slot meanwhile completes this batch itself
+    const hipEvent_t done = s.done;
+    cl.lk.unlock();
+    const hipError_t e = hipEventSynchronize(done);
+    cl.lk.lock();
+    if (e != hipSuccess) return set_err(EDV_E_HIP, "async wait", e);
+    return s.ticket == ticket ? async_complete(s) : 0;
+  }
   return 0;  // already complete (waited for, or its slot was reused)
 }
 

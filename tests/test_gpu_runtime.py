@@ -202,6 +202,44 @@ def test_host_async_path():
     assert np.array_equal(accs[4], wants[4])
 
 
+def test_host_async_path_from_threads():
+    """Three threads on one device: two queue async batches and wait (the wait
+    drops the device lock, so the other thread's submissions and the third
+    thread's synchronous calls go on meanwhile), one calls edv_verify_batch.
+    Every verdict array equals the checker."""
+    import threading
+    batches = [orc.corpus(0x7A00 + k, 0, 12000 + 977 * k, mode=k % 2, invalid_permille=120) for k in range(6)]
+    wants = [checker(*b) for b in batches]
+    errors = []
+
+    def async_worker(ks):
+        try:
+            for _ in range(3):
+                accs = {k: np.full(len(batches[k][3]) - 1, 7, np.uint8) for k in ks}
+                ts = [(k, edv.verify_async(*batches[k], accs[k])) for k in ks]
+                for k, t in ts:
+                    edv.wait_async(t)
+                    assert np.array_equal(accs[k], wants[k]), k
+        except BaseException as ex:  # reported below, in the test's thread
+            errors.append(ex)
+
+    def sync_worker():
+        try:
+            for _ in range(3):
+                assert np.array_equal(edv.verify_arrays(*batches[5]), wants[5])
+        except BaseException as ex:
+            errors.append(ex)
+
+    th = [threading.Thread(target=async_worker, args=([0, 1, 2],)),
+          threading.Thread(target=async_worker, args=([3, 4],)), threading.Thread(target=sync_worker)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in th)
+    assert errors == []
+
+
 def test_host_path_chunk_seams_with_sub_batches():
     """Small chunks: the host path's sub-batches then span several chunk-sized
     scratch regions per stream (and one stream when the chunk is tiny)."""
