@@ -60,3 +60,32 @@ def test_invalid_arguments_are_rejected_before_the_device():
     with pytest.raises(ValueError):
         edv.open_batch([(b"\0" * 64, b"", b"\0" * 31)])
     assert edv.open_batch([(b"\0" * 10, b"\0" * 10, b"\0" * 32)]) == [False]  # sm < 64: no device call
+
+
+def test_async_entry_points_validate_and_fail_loudly():
+    """edv_verify_batch_async / edv_wait_async: size mismatches are rejected in
+    the shim, a null ticket pointer and bad offsets in the C-ABI itself (before
+    any device is touched), and without a GPU a well-formed submission raises
+    EdvUnavailable rather than falling back to the CPU."""
+    import ctypes
+    from indy_plenum_amd import edv
+    sigs, pks = np.zeros(128, np.uint8), np.zeros(64, np.uint8)
+    msgs, off, acc = np.zeros(64, np.uint8), np.array([0, 16, 32], np.uint64), np.zeros(2, np.uint8)
+    with pytest.raises(ValueError):
+        edv.verify_async(sigs[:127], pks, msgs, off, acc)
+    with pytest.raises(ValueError):
+        edv.verify_async(sigs, pks, msgs, off.astype(np.int64), acc)
+    with pytest.raises(ValueError):
+        edv.verify_async(sigs, pks, msgs[:16], off, acc)
+    lib = edv.lib()
+    assert lib.edv_verify_batch_async(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, off.ctypes.data, 2,
+                                      acc.ctypes.data, 0, None) == edv.EDV_E_ARG
+    bad = np.array([0, 16, 8], np.uint64)  # offsets must not decrease
+    t = ctypes.c_int64(-1)
+    assert lib.edv_verify_batch_async(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, bad.ctypes.data, 2,
+                                      acc.ctypes.data, 0, ctypes.byref(t)) == edv.EDV_E_ARG
+    if not (os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK)):
+        with pytest.raises(edv.EdvUnavailable):
+            edv.verify_async(sigs, pks, msgs, off, acc)
+        with pytest.raises(edv.EdvUnavailable):
+            edv.wait_async(0)
