@@ -352,7 +352,9 @@ def main():
     # and gloo, since RCCL refuses two ranks on one GPU
     one_dev = os.environ.get("EDV_BENCH_ONE_DEVICE") == "1"
     dist = None
-    if world > 1:
+    # EDV_BENCH_FORCE_DIST=1 (check on a 1-GPU box): take the multi-rank path,
+    # torch.cuda + RCCL beside libedv in one process, even for one rank
+    if world > 1 or os.environ.get("EDV_BENCH_FORCE_DIST") == "1":
         import torch
         import torch.distributed as tdist
         if one_dev:

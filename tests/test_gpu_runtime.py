@@ -60,12 +60,32 @@ def _upload(*arrays):
     return bufs
 
 
+class _HipStream:
+    """A caller-owned HIP stream from the same HIP runtime libedv.so uses
+    (torch ships its own libamdhip64, a second runtime in the process)."""
+    _hip = None
+
+    def __init__(self):
+        import ctypes
+        if _HipStream._hip is None:
+            _HipStream._hip = ctypes.CDLL("libamdhip64.so.7")
+        self._s = ctypes.c_void_p()
+        assert _HipStream._hip.hipStreamCreate(ctypes.byref(self._s)) == 0
+        self.cuda_stream = self._s.value
+
+    def synchronize(self):
+        assert _HipStream._hip.hipStreamSynchronize(self._s) == 0
+
+    def __del__(self):
+        if _HipStream._hip is not None and self._s:
+            _HipStream._hip.hipStreamDestroy(self._s)
+
+
 def test_two_caller_streams_do_not_share_scratch():
     """launches on different caller streams are ordered on the
     library's scratch (st_done event), so two batches enqueued back to back on
     two streams, without any sync between them, both come out right."""
-    import torch
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    s1, s2 = _HipStream(), _HipStream()
     a = orc.corpus(0x5C1, 0, 20000, mode=0, invalid_permille=300)
     b = orc.corpus(0x5C2, 0, 30000, mode=1, invalid_permille=100)
     want_a, want_b = checker(*a), checker(*b)
