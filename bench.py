@@ -354,7 +354,13 @@ def main():
     dist = None
     # EDV_BENCH_FORCE_DIST=1 (check on a 1-GPU box): take the multi-rank path,
     # torch.cuda + RCCL beside libedv in one process, even for one rank
+    json_out = sys.stdout
     if world > 1 or os.environ.get("EDV_BENCH_FORCE_DIST") == "1":
+        # RCCL prints its version banner on stdout at communicator setup: keep
+        # the original stdout for the one JSON line, send all else to stderr
+        json_out = os.fdopen(os.dup(1), "w")
+        sys.stdout.flush()
+        os.dup2(2, 1)
         import torch
         import torch.distributed as tdist
         if one_dev:
@@ -506,7 +512,7 @@ def main():
         out["cpu_baseline"] = cb
         if cb:
             out["gpu_over_cpu"] = value / cb["value"]
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out), file=json_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
