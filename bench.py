@@ -2,28 +2,41 @@
 """Benchmark: Ed25519 verifies/s on MI355X for Plenum's client-request
 authentication hot path (BASELINE.json metric), with the INT32-VALU roofline
 fraction, rocprof-counter VALU figures, the real C-ABI boundary timed on host
-buffers, and the libsodium CPU baseline timed on the same box.
+buffers, the C4/C5 configurations, and the libsodium CPU baseline timed on the
+same box.  No PyTorch anywhere: the GPUs are driven through libedv.so only.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--reps R] [--batch B]
-                  [--msg-len 256] [--total T] [--pipeline] [--no-e2e] [--no-cpu-baseline]
+                  [--total T] [--weak] [--msg-len 256] [--pipeline] [--spawn]
+                  [--no-e2e] [--no-extra] [--no-cpu-baseline]
 
 A "step" = one pass of the verifier (prep + main kernels) over one batch of
-synthetic signed requests resident in HBM.  Default (BASELINE configs[1], C2):
-B = 65,536 NYM-shaped 256-byte messages per GPU, distinct signers, all valid;
-with N > 1 every rank verifies its own B-request shard (weak scaling).
---total T (C3, configs[2]): T requests split by request index over the ranks
-(2,097,152 per GPU at T = 16,777,216 on 8 GPUs: strong scaling), 5 % of them
-damaged (R bit, S + L, message byte, key bit) at known positions; every rank's
-accept bytes are all-gathered (RCCL) and checked against the expected verdicts.
+synthetic signed requests resident in HBM.
 
-Timing: W warm-up steps (at least --warmup-seconds of them, so a short --warmup
-gives the clocks the same settling time as a long one), then R repetitions of
-exactly K steps, each bracketed by barrier + device sync; the max over ranks of
-each repetition is taken and the MEDIAN repetition is reported.  The K steps
-of a repetition are enqueued back to back on the library stream, strictly in
-sequence (prep, main, prep, main, ...), so the kernel durations rocprofv3
-reports for the run are the ones the roofline uses.  --pipeline times the
-library's two-stream pipeline instead (prep of step k+1 beside main of step k).
+  N = 1 (default):  BASELINE configs[1] (C2): B = 65,536 NYM-shaped 256-byte
+                    messages, distinct signers, all valid.  --total T runs C3's
+                    T requests on the one GPU instead.
+  N > 1:            BASELINE configs[2] (C3): T = 16,777,216 requests per step
+                    (--total overrides), split by request index into N
+                    contiguous shards, one per GPU (strong scaling; 5 % of the
+                    requests damaged at known positions, four kinds); after the
+                    timed region every shard's accept bytes are copied (D2H) and
+                    gathered into their slices of one host array on rank 0 and
+                    checked.  --weak keeps C2's B requests per GPU instead.
+
+Processes: one per GPU.  Under torch.distributed.run (RANK / WORLD_SIZE /
+LOCAL_RANK in the environment) each rank drives device LOCAL_RANK.  Started
+directly with --gpus N > 1 (or --spawn), this script launches the N ranks
+itself, before anything touches a GPU, and only relays their exit status.  The
+ranks meet over a loopback TCP rendezvous (class Rendezvous: barrier, max of
+the per-rank times, gather of the accept bytes); there is no collective inside
+verification.
+
+Timing: W warm-up steps (at least --warmup-seconds of them), then R
+repetitions of exactly K steps, each bracketed by barrier + device sync; the
+max over ranks of each repetition is taken and the MEDIAN repetition is
+reported.  value = requests of all ranks / that time.  The K steps are enqueued
+back to back on the library stream (prep, main, prep, main, ...), so the kernel
+durations rocprofv3 reports for the run are the ones the roofline uses.
 
 The verify inputs are produced by the product's own GPU batch signer (row f-4),
 never by the oracle; only the cpu_baseline leg uses oracle/ (the libsodium
@@ -33,8 +46,12 @@ import argparse
 import json
 import os
 import platform
+import socket
 import statistics
+import struct
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -42,17 +59,30 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-from indy_plenum_amd import edv, shard, workload  # noqa: E402
+METRIC = "Ed25519 verifies/sec at 1/8 MI355X (256B msgs) + % of INT32 VALU peak vs host CPU"
+C3_TOTAL = 16777216
+C3_DAMAGE_EVERY = 20      # 5 % invalid
 
 # Algorithmic INT32 work per verify:
 #   W(m) = 217,600 + 5,500 * ceil((m + 81) / 128)   (3,400 GF(p) mul/sq x 64 u32 mul-adds + SHA-512 blocks)
 # The verify path is two launches per chunk (edv_prep_kernel, edv_main_kernel);
 # the roofline prices the whole path: W(m) per verify over the sum of both
-# kernels' HIP-event times.  (Round 1 priced the main kernel alone at
-# (2,737 + 267) x 64 ops; with half-size scalars part of that work moved into
-# prep and the rest shrank, so a per-kernel split of W would no longer mean
-# anything.)
-C3_TOTAL = 16777216
+# kernels' HIP-event times.
+# INT32 VALU peak: 256 CUs x 64 lanes/clk (4 SIMDs at the 4-cycle VOP3 rate that
+# v_mad_i64_i32 / v_mad_u64_u32 issue at, tools/ubench_valu.hip) x 2.4 GHz.
+# Plain VOP2 ops issue at twice that rate with two or more waves per SIMD
+# (MI355X_MICROARCH.md "vector-instruction ISSUE cost"): PEAK_VOP2 beside it.
+PEAK_INT32 = 256 * 64 * 2.4e9
+PEAK_VOP2 = 2 * PEAK_INT32
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
+
+
+def w_blocks(m):
+    return -(-(m + 81) // 128)
+
+
+def w_total(m):
+    return 217600 + 5500 * w_blocks(m)
 
 
 def kernel_source_hash():
@@ -65,9 +95,6 @@ def kernel_source_hash():
             h.update(f.encode())
             h.update(open(os.path.join(d, f), "rb").read())
     return h.hexdigest()
-
-
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
 
 def pmc_figures(kernels, batch, msg_len, kernel_ms):
@@ -88,13 +115,14 @@ def pmc_figures(kernels, batch, msg_len, kernel_ms):
            "traffic_source": "%s: 2 x FETCH_SIZE + WRITE_SIZE per launch, prep + main (gfx950 correction; "
                              "Infinity-Cache (MALL) hits included, so an upper bound on DRAM bytes)"
                              % os.path.relpath(PMC_SUMMARY, ROOT)}
+    for key in ("dram_bytes_per_launch_bound", "dram_note"):
+        if key in s:
+            out[key] = s[key]
     cs = [k["counters"] for k in ks]
     if all("SQ_INSTS_VALU" in c for c in cs):
         valu = sum(c["SQ_INSTS_VALU"] for c in cs)  # wave-instructions per launch pair
         lane_ops = valu * 64  # one lane-op per active lane per VALU wave-instruction
         out.update({
-            # a verify is one lane in each kernel (and in each prep side): per-lane
-            # instructions = wave-instructions x 64 lanes / verifies
             "valu_insts_per_verify": valu * 64 / batch,
             "valu_int64_insts_per_verify": sum(c.get("SQ_INSTS_VALU_INT64", 0.0) for c in cs) * 64 / batch,
             "valu_int32_insts_per_verify": sum(c.get("SQ_INSTS_VALU_INT32", 0.0) for c in cs) * 64 / batch,
@@ -102,23 +130,11 @@ def pmc_figures(kernels, batch, msg_len, kernel_ms):
             "measured_valu_frac_of_issue_peak": lane_ops / (kernel_ms * 1e-3) / PEAK_INT32,
             "per_kernel": {name: {"valu_insts_per_wave": k.get("valu_insts_per_wave"), "waves": k["counters"].get("SQ_WAVES"),
                                   "valu_busy": k.get("valu_busy"), "wave_cycle_split": k.get("wave_cycle_split"),
-                                  "hbm_bytes_per_launch": k.get("hbm_bytes_per_launch")}
+                                  "hbm_bytes_per_launch": k.get("hbm_bytes_per_launch"),
+                                  "l2_hit_rate": k.get("l2_hit_rate")}
                            for name, k in zip(kernels, ks)},
         })
     return out, None
-
-
-def w_total(m):
-    return 217600 + 5500 * -(-(m + 81) // 128)
-
-
-# INT32 VALU peak: 256 CUs x 64 lanes/clk (4 SIMDs at the 4-cycle VOP3 rate that
-# v_mad_i64_i32 / v_mad_u64_u32 issue at, tools/ubench_valu.hip) x 2.4 GHz.
-# Plain VOP2 ops (v_add_u32, v_xor_b32, ...) issue at twice that rate with two or
-# more waves per SIMD (MI355X_MICROARCH.md "vector-instruction ISSUE cost"):
-# PEAK_VOP2 is reported beside it.
-PEAK_INT32 = 256 * 64 * 2.4e9
-PEAK_VOP2 = 2 * PEAK_INT32
 
 
 def cpu_info():
@@ -132,13 +148,160 @@ def cpu_info():
     except OSError:
         pass
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
-    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "model": model,
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota, "model": model,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
+# ------------------------------------------------------------------ ranks
+class Rendezvous:
+    """The ranks of one bench run on one node, over loopback TCP: rank 0
+    listens on an ephemeral port it publishes in a file named by a token all
+    ranks share (the launcher's, or torch.distributed.run's agent pid and
+    MASTER_PORT); the others connect.  Collectives are synchronous: every rank
+    sends, rank 0 answers.  Used only outside the timed region and for the
+    barriers around it."""
+
+    def __init__(self, rank, world, token, timeout=900.0):
+        self.rank, self.world, self.peers, self.sock = rank, world, [], None
+        if world == 1:
+            return
+        path = os.path.join(tempfile.gettempdir(), "edv_bench_%s.port" % token)
+        deadline = time.time() + timeout
+        if rank == 0:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.bind(("127.0.0.1", 0))
+            srv.listen(world)
+            tmp = path + ".tmp%d" % os.getpid()
+            with open(tmp, "w") as f:
+                f.write(str(srv.getsockname()[1]))
+            os.replace(tmp, path)
+            srv.settimeout(timeout)
+            peers = {}
+            try:
+                while len(peers) < world - 1:
+                    c, _ = srv.accept()
+                    c.settimeout(timeout)
+                    peers[struct.unpack("<I", self._recvn(c, 4))[0]] = c
+            finally:
+                srv.close()
+                try:
+                    os.unlink(path)
+                except OSError:
+                    pass
+            self.peers = [peers[r] for r in range(1, world)]
+        else:
+            while True:
+                try:
+                    with open(path) as f:
+                        port = int(f.read())
+                    self.sock = socket.create_connection(("127.0.0.1", port), timeout=10)
+                    break
+                except (OSError, ValueError):
+                    if time.time() > deadline:
+                        raise RuntimeError("rank %d: no rendezvous with rank 0 (%s)" % (rank, path))
+                    time.sleep(0.05)
+            self.sock.settimeout(timeout)
+            self.sock.sendall(struct.pack("<I", rank))
+
+    @staticmethod
+    def _recvn(s, n):
+        buf = bytearray()
+        while len(buf) < n:
+            b = s.recv(min(n - len(buf), 1 << 20))
+            if not b:
+                raise RuntimeError("bench rendezvous: a rank went away")
+            buf += b
+        return bytes(buf)
+
+    def _send(self, s, payload):
+        s.sendall(struct.pack("<Q", len(payload)) + payload)
+
+    def _recv(self, s):
+        return self._recvn(s, struct.unpack("<Q", self._recvn(s, 8))[0])
+
+    def gather(self, payload, broadcast=True):
+        """Every rank's payload (bytes), in rank order, on rank 0 (and on every
+        rank when broadcast)."""
+        if self.world == 1:
+            return [payload]
+        if self.rank == 0:
+            got = [payload] + [self._recv(c) for c in self.peers]
+            if broadcast:
+                blob = b"".join(struct.pack("<Q", len(g)) + g for g in got)
+                for c in self.peers:
+                    self._send(c, blob)
+            return got
+        self._send(self.sock, payload)
+        if not broadcast:
+            return None
+        blob, out, p = self._recv(self.sock), [], 0
+        while p < len(blob):
+            k = struct.unpack_from("<Q", blob, p)[0]
+            out.append(blob[p + 8:p + 8 + k])
+            p += 8 + k
+        return out
+
+    def barrier(self):
+        self.gather(b"")
+
+    def max(self, x):
+        return max(struct.unpack("<d", g)[0] for g in self.gather(struct.pack("<d", x)))
+
+    def close(self):
+        for c in self.peers + ([self.sock] if self.sock else []):
+            try:
+                c.close()
+            except OSError:
+                pass
+
+
+def launch_ranks(n):
+    """Start N ranks of this script (RANK / LOCAL_RANK / WORLD_SIZE set, device
+    = LOCAL_RANK) before anything here touches a GPU; relay their exit status.
+    If one rank fails, the others are stopped (by their PIDs) instead of
+    waiting at the next barrier."""
+    token = "l%d_%d" % (os.getpid(), time.time_ns())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   EDV_BENCH_TOKEN=token)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.kill()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 1
+
+
+def rank_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    token = os.environ.get("EDV_BENCH_TOKEN") or "t%d_%s" % (os.getppid(), os.environ.get("MASTER_PORT", "0"))
+    return world, rank, local, token
+
+
+# --------------------------------------------------------------- CPU baseline
 def cpu_baseline(batch, budget_s):
-    """libsodium 1.0.18 verify_detached over the same batch on the host cores,
-    plus the reference's single-threaded Python chain (C1)."""
+    """libsodium 1.0.18 verify_detached over the same batch on the host cores:
+    all the cores this process may run on, the box's 16-CPU share, and one
+    thread; plus the reference's single-threaded Python chain on C1 (10k)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as orc  # the baseline leg is the only oracle/ user here
     sb = orc.sodium_batch()
@@ -147,25 +310,33 @@ def cpu_baseline(batch, budget_s):
     sigs, pks, msgs, off = batch.host_copy()
     info = cpu_info()
     ncpu = info["affinity_cpus"] or info["nproc"] or 1
-    # the GPU box's CPU share for one GPU is 16 threads (OMP_NUM_THREADS there);
-    # the machine's nproc counts every CPU of the host, shared with other jobs
-    threads = max(1, min(16, ncpu))
-    acc = orc.sodium_verify_batch(sigs, pks, msgs, off, threads)  # warm + sanity
-    assert acc.all()
     n = batch.n
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        orc.sodium_verify_batch(sigs, pks, msgs, off, threads)
-        done += n
-    dt = time.perf_counter() - t0
+    acc = orc.sodium_verify_batch(sigs, pks, msgs, off, min(16, ncpu))  # warm + sanity
+    assert np.array_equal(acc, batch.expected())
+
+    def rate(threads, seconds):
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            orc.sodium_verify_batch(sigs, pks, msgs, off, threads)
+            done += n
+        dt = time.perf_counter() - t0
+        return done / dt, done // n, dt
+
+    all_threads = min(512, ncpu)
+    v_all, p_all, t_all = rate(all_threads, budget_s)
+    share = min(16, ncpu)
+    v_share, p_share, t_share = rate(share, budget_s / 2) if share != all_threads else (v_all, p_all, t_all)
     k = min(n, 16384)
     t1 = time.perf_counter()
     orc.sodium_verify_batch(sigs[:64 * k], pks[:32 * k], msgs, off[:k + 1], 1)
     one = k / (time.perf_counter() - t1)
-    out = {"value": done / dt, "unit": "verifies/s", "cores": threads, "kind": "reference",
+    out = {"value": v_all, "unit": "verifies/s", "cores": all_threads, "kind": "reference",
            "sample": "%d passes over the %d-request batch (%d B msgs): libsodium %s crypto_sign_ed25519_verify_detached "
-                     "(oracle/sodium_batch.c), %d threads, %.1f s" % (done // n, n, int(off[1] - off[0]),
-                                                                      sb.sb_version().decode(), threads, dt),
+                     "(oracle/sodium_batch.c), %d threads = every CPU this process may use, %.1f s"
+                     % (p_all, n, int(off[1] - off[0]), sb.sb_version().decode(), all_threads, t_all),
+           "all_cores_verifies_per_s": v_all, "all_cores_threads": all_threads,
+           "share_verifies_per_s": v_share, "share_threads": share,
+           "share_sample": "%d passes, %.1f s (16 threads: the box's CPU share per GPU)" % (p_share, t_share),
            "one_thread_verifies_per_s": one, "host": info}
     try:
         out["c1_python_chain"] = c1_chain()
@@ -176,21 +347,19 @@ def cpu_baseline(batch, budget_s):
 
 def c1_requests(n, seed=0xC1):
     """C1: NYM-style requests, distinct signers, identifier = b58(pk[:16]) and
-    verkey '~' + b58(pk[16:]) registered, signed (GPU batch signer) over their
-    SigningSerializer bytes (~150 B)."""
-    from indy_plenum_amd import base58
-    from indy_plenum_amd.client_authn import CoreAuthNr
+    verkey '~' + b58(pk[16:]), signed (GPU batch signer) over their
+    SigningSerializer bytes (~150 B).  -> (verkeys {idr: '~...'}, reqs)."""
+    from indy_plenum_amd import base58, edv
     from indy_plenum_amd.signing_serializer import serialize_msg_for_signing
     rng = np.random.default_rng(seed)
     seeds = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
     pks, _ = edv.sign_arrays(seeds.tobytes(), b"\0" * 64, np.zeros(n + 1, dtype=np.uint64))
     pks = np.frombuffer(pks, np.uint8).reshape(n, 32)
-    auth = CoreAuthNr()
-    reqs = []
+    verkeys, reqs = {}, []
     for i in range(n):
         pk = pks[i].tobytes()
         idr = base58.b58encode(pk[:16]).decode()
-        auth.addIdr(idr, "~" + base58.b58encode(pk[16:]).decode())
+        verkeys[idr] = "~" + base58.b58encode(pk[16:]).decode()
         reqs.append({"identifier": idr, "reqId": 1539648000000000 + i, "protocolVersion": 2,
                      "operation": {"type": "1", "dest": base58.b58encode(rng.bytes(16)).decode(),
                                    "verkey": "~" + base58.b58encode(rng.bytes(16)).decode()}})
@@ -201,10 +370,10 @@ def c1_requests(n, seed=0xC1):
     sigs = sigs.tobytes()
     for i, r in enumerate(reqs):
         r["signature"] = base58.b58encode(sigs[64 * i:64 * i + 64]).decode()
-    return auth, reqs
+    return verkeys, reqs
 
 
-def c1_chain(n=3000):
+def c1_chain(n=10000):
     """The reference's CPU chain on C1: sequential CoreAuthNr.authenticate per
     request, Python restatement of P1-P7 + libsodium crypto_sign_open via ctypes
     (what libnacl does), one thread like the Node's Looper; native base58 and
@@ -215,9 +384,10 @@ def c1_chain(n=3000):
     from indy_plenum_amd.client_authn import CoreAuthNr
     if sodium_ref.sodium() is None:
         return {"error": "libsodium not found"}
-    auth, reqs = c1_requests(n)
+    verkeys, reqs = c1_requests(n)
     cpu = CoreAuthNr()
-    cpu.clients = auth.clients
+    for idr, vk in verkeys.items():
+        cpu.addIdr(idr, vk)
     saved = base58._native, signing_serializer._native
     base58._native = signing_serializer._native = None
     try:
@@ -232,6 +402,7 @@ def c1_chain(n=3000):
                     "via ctypes, 1 thread"}
 
 
+# ------------------------------------------------------------- other legs
 def median_time(f, reps):
     ts = []
     for _ in range(reps):
@@ -244,7 +415,8 @@ def median_time(f, reps):
 def e2e_leg(batch, device_value, reps=5):
     """The drop-in boundary itself: edv_verify_batch on HOST buffers (H2D, kernels,
     D2H, synchronous), pageable numpy arrays and pinned (edv_host_alloc) arrays,
-    median of `reps` calls each."""
+    median of `reps` calls each; and back to back through edv_verify_batch_async."""
+    from indy_plenum_amd import edv
     sigs, pks, msgs, off = batch.host_copy()
     n = batch.n
     want = batch.expected()
@@ -257,7 +429,6 @@ def e2e_leg(batch, device_value, reps=5):
     call(sigs, pks, msgs, off, acc)  # warm: buffers sized, pinned staging allocated
     assert np.array_equal(acc, want)
     t_page = median_time(lambda: call(sigs, pks, msgs, off, acc), reps)
-    # pinned: pack the same arrays into one page-locked arena
     sizes = [sigs.nbytes, pks.nbytes, off.nbytes, msgs.nbytes, n]
     pb = edv.PinnedBuffer(sum(sizes) + 5 * 64)
     views, pos = [], 0
@@ -272,8 +443,6 @@ def e2e_leg(batch, device_value, reps=5):
     call(ps, pp, pm, po, pa)
     assert np.array_equal(pa, want)
     t_pin = median_time(lambda: call(ps, pp, pm, po, pa), reps)
-    # back to back through edv_verify_batch_async: batch k+1's copies run while
-    # batch k computes (two verdict arrays in turn, waits one batch behind)
     pa2 = np.zeros(n, np.uint8)
     k_async = 10
 
@@ -307,12 +476,31 @@ def e2e_leg(batch, device_value, reps=5):
             "pcie_bytes_per_call": int(sigs.nbytes + pks.nbytes + off.nbytes + int(off[-1] - off[0]) + n)}
 
 
+class DictState:
+    """A state with the reference's get(key, isCommitted) contract
+    (PruningState.get, state/pruning_state.py), held in a dict: the NYM values
+    of the state-backed node_path population.  A dict read is cheaper than the
+    reference's trie + KV read, so this times everything but the storage."""
+
+    def __init__(self):
+        self.kv = {}
+
+    def get(self, key, isCommitted=True):
+        return self.kv.get(key)
+
+
 def node_path_leg(n=65536, reps=3):
     """f-1: CoreAuthNr.authenticate_batch over n C1-shaped requests on this GPU
-    (native host prep, one verify call, replay)."""
-    from indy_plenum_amd import _edvhost
+    (native host prep, one verify call, replay), with the verkeys (a) in the
+    in-memory clients map and (b) only in the uncommitted state
+    (client_authn.py:148-160, the NYMs not yet committed)."""
+    from indy_plenum_amd import _edvhost, edv
+    from indy_plenum_amd.client_authn import CoreAuthNr, nym_to_state_key
     from indy_plenum_amd.req_authenticator import ReqAuthenticator
-    auth, reqs = c1_requests(n, seed=0xF1)
+    verkeys, reqs = c1_requests(n, seed=0xF1)
+    auth = CoreAuthNr()
+    for idr, vk in verkeys.items():
+        auth.addIdr(idr, vk)
     res = auth.authenticate_batch(reqs)
     assert all(x == [r["identifier"]] for x, r in zip(res, reqs))
     t = median_time(lambda: auth.authenticate_batch(reqs), reps)
@@ -321,75 +509,151 @@ def node_path_leg(n=65536, reps=3):
     ra.register_authenticator(auth)
     assert all(x == {r["identifier"]} for x, r in zip(ra.authenticate_batch(reqs), reqs))
     t_ra = median_time(lambda: ra.authenticate_batch(reqs), reps)
+    st = DictState()
+    for idr, vk in verkeys.items():
+        st.kv[nym_to_state_key(idr)] = json.dumps({"verkey": vk, "role": None}).encode()
+    sauth = CoreAuthNr(state=st)
+    calls = []
+    real = edv.open_batch
+
+    def counting(items, device_mask=0):   # requests the native path handed back to the Python plan
+        items = list(items)
+        calls.append(len(items))
+        return real(items, device_mask)
+    edv.open_batch = edv._OPEN_BATCH = counting   # both: the native path stays enabled
+    try:
+        res = sauth.authenticate_batch(reqs)
+    finally:
+        edv.open_batch = edv._OPEN_BATCH = real
+    assert all(x == [r["identifier"]] for x, r in zip(res, reqs))
+    t_st = median_time(lambda: sauth.authenticate_batch(reqs), reps)
     return {"what": "CoreAuthNr.authenticate_batch, %d NYM requests (~150 B signing bytes), 1 GPU, median of %d; "
                     "native host prep on %d threads" % (n, reps, edv.PREP_THREADS),
             "requests_per_s": n / t, "ms": 1e3 * t, "phases_last_call_s": phases,
-            "req_authenticator_requests_per_s": n / t_ra}
+            "req_authenticator_requests_per_s": n / t_ra,
+            "state_backed": {"requests_per_s": n / t_st, "ms": 1e3 * t_st,
+                             "native_path_hit_rate": 1.0 - sum(calls) / n,
+                             "what": "the same requests with no clients entries: every verkey read from the "
+                                     "uncommitted state (dict-backed get(key, isCommitted=False)); state keys by "
+                                     "one GPU SHA-256 batch"}}
 
 
-def main():
+def timed_steps(step, drain, steps, reps, rdv):
+    """R repetitions of `steps` steps, each between barrier + sync; max over
+    ranks per repetition -> list of seconds."""
+    out = []
+    for _ in range(max(1, reps)):
+        drain()
+        rdv.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        drain()
+        t1 = time.perf_counter()
+        rdv.barrier()
+        out.append(rdv.max(t1 - t0))
+    return out
+
+
+def c4_leg(dev, steps, reps, n=65536):
+    """C4 (BASELINE configs[3]): n requests of 200..4,096 B (length-bucketed
+    SHA-512), 5 % invalid over seven kinds (R bit, S + L, message byte, key bit,
+    small-order R, non-canonical A, small-order A), device resident; verdicts
+    checked against the construction."""
+    from indy_plenum_amd import edv, workload
+    b = workload.DeviceBatch(n, device=dev, seed=0xC4C4, var_range=(200, 4096), damage_every=20, damage_kinds=7,
+                             keep_host=False)
+    b.verify()
+    got = b.accept()
+    exp = b.expected()
+    ok = bool(np.array_equal(got, exp))
+    for _ in range(3):
+        b.verify(stream=edv.stream(dev))
+    edv.sync(dev)
+    rdv = Rendezvous(0, 1, "")
+    s = edv.stream(dev)
+    ts = timed_steps(lambda: b.verify(stream=s), lambda: edv.sync(dev), steps, reps, rdv)
+    el = statistics.median(ts)
+    lens = np.diff(b.host_off).astype(np.int64)
+    ops = float(np.sum(217600 + 5500 * ((lens + 81 + 127) // 128)))
+    prep_ms, main_ms = edv.profile_device(b.d_sigs.ptr, b.d_pks.ptr, b.d_msgs.ptr, b.d_off.ptr, n, b.d_accept.ptr,
+                                          dev, max(3, min(steps, 10)))
+    return {"workload": "C4: %d Ed25519 verifies per step, messages uniform in 200..4,096 B (mean %.0f B), "
+                        "length-bucketed SHA-512, 5 %% invalid over %s" % (n, lens.mean(), ", ".join(workload.DAMAGE_KINDS)),
+            "verifies_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps, "reps_s": ts,
+            "verdicts_as_expected": ok, "invalid": int(n - exp.sum()),
+            "prep_kernel_ms": prep_ms, "main_kernel_ms": main_ms,
+            "roofline_frac": ops / ((prep_ms + main_ms) * 1e-3) / PEAK_INT32,
+            "w_ops_per_verify_mean": ops / n}
+
+
+def c5_leg(n=20000, n_cpu=2000):
+    """C5 (BASELINE configs[4]): the 4-node pool (Alpha..Delta) under a client
+    flood with the GPU verify_batch behind ReqAuthenticator, against the
+    reference's one-message-at-a-time flow on libsodium (tools/bench_pool.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_pool
+    out = bench_pool.c5(n, n_cpu)
+    g = out["gpu_batched"]
+    out["summary"] = {"gpu_ordered_req_per_s": g["ordered_req_per_s_one_process"],
+                      "gpu_auth_share_of_node_time": g["auth_share_of_node_time"],
+                      "cpu_ordered_req_per_s": out.get("cpu_reference", {}).get("ordered_req_per_s_one_process"),
+                      "cpu_auth_share_of_node_time": out.get("cpu_reference", {}).get("auth_share_of_node_time")}
+    return out
+
+
+# --------------------------------------------------------------------- main
+def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5, help="untimed steps first (at least --warmup-seconds of them)")
     ap.add_argument("--warmup-seconds", type=float, default=1.0)
     ap.add_argument("--reps", type=int, default=5, help="timed repetitions of --steps steps; the median is reported")
-    ap.add_argument("--batch", type=int, default=65536, help="requests per GPU per step (C2)")
+    ap.add_argument("--batch", type=int, default=65536, help="C2: requests per GPU per step")
     ap.add_argument("--total", type=int, default=0,
-                    help="C3: total requests per step, split by request index over the ranks (e.g. %d)" % C3_TOTAL)
+                    help="C3: total requests per step split by request index over the GPUs "
+                         "(default %d when --gpus > 1)" % C3_TOTAL)
+    ap.add_argument("--weak", action="store_true", help="with --gpus > 1: C2's --batch per GPU instead of C3")
     ap.add_argument("--msg-len", type=int, default=256)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer boundary and node-path legs")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C4 and C5 legs")
+    ap.add_argument("--spawn", action="store_true", help="launch the ranks from this process even for one GPU")
     ap.add_argument("--pipeline", action="store_true",
                     help="time the two-stream pipelined submission (prep of step k+1 beside main of step k)")
-    args = ap.parse_args()
+    return ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # EDV_BENCH_ONE_DEVICE=1 (rehearsal on a 1-GPU box only): every rank uses device 0
-    # and gloo, since RCCL refuses two ranks on one GPU
-    one_dev = os.environ.get("EDV_BENCH_ONE_DEVICE") == "1"
-    dist = None
-    # EDV_BENCH_FORCE_DIST=1 (check on a 1-GPU box): take the multi-rank path,
-    # torch.cuda + RCCL beside libedv in one process, even for one rank
-    json_out = sys.stdout
-    if world > 1 or os.environ.get("EDV_BENCH_FORCE_DIST") == "1":
-        # RCCL prints its version banner on stdout at communicator setup: keep
-        # the original stdout for the one JSON line, send all else to stderr
-        json_out = os.fdopen(os.dup(1), "w")
-        sys.stdout.flush()
-        os.dup2(2, 1)
-        import torch
-        import torch.distributed as tdist
-        if one_dev:
-            tdist.init_process_group("gloo")
-        else:
-            torch.cuda.set_device(local)
-            tdist.init_process_group("nccl")  # RCCL over xGMI
-        dist = tdist
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
+def main():
+    args = parse_args()
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.spawn):
+        sys.exit(launch_ranks(args.gpus))
+    world, rank, local, token = rank_env()
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
 
-    def max_over_ranks(x):
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64, device="cpu" if one_dev else "cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+    from indy_plenum_amd import edv, shard, workload
+    ndev = edv.device_count()
+    if local >= ndev:
+        sys.exit("bench.py: rank %d needs device %d, but %d gfx950 device(s) are visible (--gpus %d)"
+                 % (rank, local, ndev, args.gpus))
+    dev = local
+    rdv = Rendezvous(rank, world, token)
 
-    dev = 0 if one_dev else local
-    c3 = args.total > 0
+    c3 = args.total > 0 or (world > 1 and not args.weak)
+    total = (args.total or C3_TOTAL) if c3 else args.batch * world
     if c3:
-        lo, hi = shard.shard_range(args.total, world, rank)   # one message length: equal counts
-        n, start, damage = hi - lo, lo, 20
+        lo, hi = shard.shard_range(total, world, rank)   # one message length: equal counts
+        n, start, damage = hi - lo, lo, C3_DAMAGE_EVERY
     else:
         n, start, damage = args.batch, rank * args.batch, 0
+    t_gen = time.perf_counter()
     batch = workload.DeviceBatch(n, device=dev, start=start, msg_len=args.msg_len, damage_every=damage)
+    t_gen = time.perf_counter() - t_gen
+
+    s = edv.stream(dev)
 
     def step():
         if args.pipeline:
@@ -403,7 +667,6 @@ def main():
         else:
             edv.sync(dev)
 
-    s = edv.stream(dev)
     t0, done = time.perf_counter(), 0
     while done < args.warmup or time.perf_counter() - t0 < args.warmup_seconds:
         step()
@@ -412,25 +675,12 @@ def main():
             drain()
     drain()
     warm_steps = done
-    ok = batch.accept()
-    assert np.array_equal(ok, batch.expected()), "warm-up verdicts differ from the expected ones"
+    assert np.array_equal(batch.accept(), batch.expected()), "warm-up verdicts differ from the expected ones"
 
-    def timed():
-        drain()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        drain()
-        t1 = time.perf_counter()
-        barrier()
-        return max_over_ranks(t1 - t0)
-
-    reps = [timed() for _ in range(max(1, args.reps))]
+    reps = timed_steps(step, drain, args.steps, args.reps, rdv)
     elapsed = statistics.median(reps)
     ms_step = 1e3 * elapsed / args.steps
-    total = n * world * args.steps
-    value = total / elapsed
+    value = total * args.steps / elapsed
 
     # per-kernel durations (HIP events on the kernels' own stream) on the first
     # chunk-sized slice of this rank's batch
@@ -438,26 +688,26 @@ def main():
     iters = max(3, min(args.steps, 10))
     prep_ms, main_ms = edv.profile_device(batch.d_sigs.ptr, batch.d_pks.ptr, batch.d_msgs.ptr, batch.d_off.ptr, pn,
                                           batch.d_accept.ptr, dev, iters)
+    # untimed: every rank verifies once more, copies its accept bytes D2H and
+    # sends them to rank 0, which places each in its slice of one host array
     batch.verify()
-    ok = batch.accept()
-    if dist is not None:
-        # untimed: gather every shard's accept bytes back into request order (RCCL all-gather)
-        sys.path.insert(0, os.path.join(ROOT, "tools"))
-        import torch
-        from dist_gather import gather_accept
-        bounds = ([shard.shard_range(args.total, world, r)[0] for r in range(world)] + [args.total] if c3
-                  else [r * n for r in range(world + 1)])
-        exp = np.ones(bounds[-1], np.uint8)
-        exp[workload.damage_positions(0, bounds[-1], damage)] = 0
-        full = gather_accept(dist, ok, bounds, device=None if one_dev else torch.device("cuda", local))
+    mine = batch.accept()
+    parts = rdv.gather(mine.tobytes(), broadcast=False)
+    verdicts_ok = None
+    if rank == 0:
+        full = np.empty(total, np.uint8)
+        bounds = ([shard.shard_range(total, world, r)[0] for r in range(world)] + [total] if c3
+                  else [r * args.batch for r in range(world + 1)])
+        for r, p in enumerate(parts):
+            full[bounds[r]:bounds[r + 1]] = np.frombuffer(p, np.uint8)
+        exp = np.ones(total, np.uint8)
+        exp[workload.damage_positions(0, total, damage)] = 0
         verdicts_ok = bool(np.array_equal(full, exp))
-    else:
-        verdicts_ok = bool(np.array_equal(ok, batch.expected()))
-
+    rdv.barrier()
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
+        rdv.close()
         return
+
     path_ms = prep_ms + main_ms
     ops = w_total(args.msg_len) * pn
     achieved = ops / (path_ms * 1e-3)
@@ -472,8 +722,19 @@ def main():
                               "kernel time); peak = 256 CU x 64 lanes x 2.4 GHz (4-cycle VOP3 issue)"}
     if pmc:
         roofline.update(pmc)
+    if c3:
+        config = {"workload": "C3: %d Ed25519 verifies per step split by request index over %d GPU(s) (%d per GPU), "
+                              "fixed %d-byte serialized requests, 5 %% invalid, accept bytes gathered to host and "
+                              "checked" % (total, world, n, args.msg_len),
+                  "total_per_step": total, "per_gpu": n, "msg_len": args.msg_len,
+                  "parallelism": "shard-by-request-index x%d (one process per GPU)" % world}
+    else:
+        config = {"workload": "C2: %d Ed25519 verifies per GPU per step, fixed %d-byte serialized requests, distinct "
+                              "signers%s" % (n, args.msg_len, "" if world == 1 else "; shard by request index"),
+                  "batch_per_gpu": n, "msg_len": args.msg_len,
+                  "parallelism": "shard-by-request-index x%d (one process per GPU)" % world}
     out = {
-        "metric": "Ed25519 verifies/sec (256B msgs) + % of INT32 VALU peak",
+        "metric": METRIC,
         "value": value,
         "unit": "verifies/s",
         "n_gpus": world,
@@ -485,21 +746,16 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic: NYM-shaped signing bytes, distinct signers, keys+signatures made by the GPU batch signer"
-                + ("; 5%% damaged at known positions" if c3 else ""),
-        "config": ({"workload": "C3: %d Ed25519 verifies per step split by request index over %d GPU(s) (%d per GPU), "
-                                "fixed %d-byte serialized requests, accept bytes all-gathered and checked"
-                                % (args.total, world, n, args.msg_len),
-                    "total_per_step": args.total, "per_gpu": n, "msg_len": args.msg_len,
-                    "parallelism": "shard-by-request-index x%d" % world} if c3 else
-                   {"workload": "C2: %d Ed25519 verifies per GPU per step, fixed %d-byte serialized requests, distinct "
-                                "signers%s" % (n, args.msg_len, "" if world == 1 else "; shard by request index"),
-                    "batch_per_gpu": n, "msg_len": args.msg_len, "parallelism": "shard-by-request-index x%d" % world}),
+                + ("; 5% damaged at known positions (R bit, S + L, message byte, key bit)" if c3 else ""),
+        "config": config,
         "roofline": roofline,
         "verdicts_as_expected": verdicts_ok,
         "timing": {"mode": "pipelined (prep of step k+1 beside main of step k)" if args.pipeline else "sequential",
                    "reps_s": reps, "median_of": len(reps), "warmup_steps_run": warm_steps,
-                   "kernel_sum_ms": prep_ms + main_ms,
-                   "gap_ms_per_step": ms_step - (prep_ms + main_ms) * n / pn},
+                   "kernel_sum_ms": path_ms, "gap_ms_per_step": ms_step - path_ms * n / pn,
+                   "launch": "ranks started by bench.py" if os.environ.get("EDV_BENCH_TOKEN") else
+                             ("torch.distributed.run ranks" if world > 1 else "single process"),
+                   "input_generation_s": t_gen},
     }
     if world == 1 and not c3 and not args.no_e2e:
         out["e2e"] = e2e_leg(batch, value)
@@ -507,14 +763,20 @@ def main():
             out["node_path"] = node_path_leg()
         except Exception as ex:
             out["node_path"] = {"error": repr(ex)}
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not c3 and not args.no_extra:
+        for name, leg in (("c4", lambda: c4_leg(dev, args.steps, args.reps)), ("c5", c5_leg)):
+            try:
+                out[name] = leg()
+            except Exception as ex:
+                out[name] = {"error": repr(ex)}
+    if world == 1 and not c3 and not args.no_cpu_baseline:
         cb = cpu_baseline(batch, args.cpu_seconds)
         out["cpu_baseline"] = cb
         if cb:
             out["gpu_over_cpu"] = value / cb["value"]
-    print(json.dumps(out), file=json_out, flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+            out["gpu_over_cpu_share"] = value / cb["share_verifies_per_s"]
+    print(json.dumps(out), flush=True)
+    rdv.close()
 
 
 if __name__ == "__main__":

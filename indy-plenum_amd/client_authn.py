@@ -359,7 +359,52 @@ class CoreAuthMixin:
         if not self._stock(verifier) or not edv.native_batch_enabled():
             return None
         return _edvhost.auth_core_batch(reqs, self.clients, self.excluded_from_signing, edv.verify_address(),
-                                        edv.BATCH_DEVICE_MASK, edv.PREP_THREADS)
+                                        edv.BATCH_DEVICE_MASK, edv.PREP_THREADS, self._state_nyms(reqs))
+
+    # below this many state keys hashlib beats a device round trip
+    STATE_KEYS_ON_DEVICE = 512
+
+    def _state_nyms(self, reqs):
+        """The NYMs getVerkey would read from the uncommitted state for this
+        batch (client_authn.py:148-160 -> domain_req_handler.py:158-167): every
+        string identifier whose `clients` entry is missing or falsy.  Their state
+        keys (nym_to_state_key) come from one SHA-256 batch (row f-3), then one
+        state.get(key, isCommitted=False) each, as the reference does per
+        request.  -> {identifier: nym dict} holding non-empty dicts only (any
+        other value -- absent, empty, not a JSON object -- stays with the Python
+        plan, which raises what the reference raises), or None without a state."""
+        state = self.state
+        if state is None:
+            return None
+        clients = self.clients
+        idrs = []
+        seen = set()
+        for r in reqs:
+            if type(r) is dict:
+                i = r.get(IDENTIFIER)
+                if type(i) is str and i and i not in seen and not clients.get(i):
+                    seen.add(i)
+                    idrs.append(i)
+        if not idrs:
+            return None
+        if len(idrs) >= self.STATE_KEYS_ON_DEVICE:
+            from .digest import nym_state_keys
+            keys = nym_state_keys(idrs)
+        else:
+            keys = [nym_to_state_key(i) for i in idrs]
+        out = {}
+        loads = json.loads
+        for i, key in zip(idrs, keys):
+            data = state.get(key, False)
+            if not data:
+                continue
+            try:
+                nym = loads(bytes(data).decode() if isinstance(data, (bytes, bytearray)) else data)
+            except Exception:
+                continue
+            if type(nym) is dict and nym:
+                out[i] = nym
+        return out
 
     # requests are only read, never mutated, by the stock batch path above
     def batch_reads_only(self):

@@ -487,12 +487,14 @@ PyObject* py_prep_core_batch(PyObject*, PyObject* args) {
 }
 
 // --------------------------------------------- whole-batch CoreAuthNr (f-1)
-// auth_core_batch(reqs, clients, excluded, verify_addr, device_mask, threads)
+// auth_core_batch(reqs, clients, excluded, verify_addr, device_mask, threads[, resolved])
 //   -> (out, slow, rejected)
 // The single-signature fast path of prep_core_batch, done for a whole batch in
 // one call with the GPU verify inside it:
-//   phase A (GIL held)  type checks, in-memory verkey lookup (SimpleAuthNr.getVerkey,
-//                       client_authn.py:148-160), SigningSerializer bytes
+//   phase A (GIL held)  type checks, verkey lookup (SimpleAuthNr.getVerkey,
+//                       client_authn.py:148-160: the in-memory map, else the NYM
+//                       the caller read from the uncommitted state, `resolved`),
+//                       SigningSerializer bytes
 //                       (client_authn.py:248-252) appended to the message arena;
 //   phase B (no GIL)    base58 of signatures, identifiers and verkeys
 //                       (client_authn.py:94, verifier.py:26-52) on `threads`
@@ -582,24 +584,44 @@ inline bool ascii_str(PyObject* o, const uint8_t** p, size_t* n) {
 // phase A for one request: false = not the fast path (nothing appended)
 PyObject *g_k_identifier, *g_k_signature, *g_k_verkey;  // interned key strings (module init)
 
-int collect_one(PyObject* req, PyObject* clients, PyObject* excluded, Py_ssize_t k, std::string& msgs,
-                FastItem* it) {
+// verkey source of one identifier, as SimpleAuthNr.getVerkey (client_authn.py:148-160)
+// reads it: the in-memory `clients` entry unless it is falsy, else the NYM the
+// caller resolved from the uncommitted state (`resolved`: identifier -> nym dict,
+// holding only non-empty dicts; None when the authenticator has no state).
+// 1 = *nym set (a non-empty exact dict), 0 = not the fast path, -1 = error.
+int lookup_nym(PyObject* clients, PyObject* resolved, PyObject* idr, PyObject** nym) {
+  PyObject* v = PyDict_GetItemWithError(clients, idr);
+  if (!v && PyErr_Occurred()) return -1;
+  if (v && PyDict_CheckExact(v) && PyDict_GET_SIZE(v) > 0) { *nym = v; return 1; }
+  // present but truthy and not a plain dict: the reference calls its .get (Python plan)
+  if (v && v != Py_None && !(PyDict_CheckExact(v) && PyDict_GET_SIZE(v) == 0)) return 0;
+  if (resolved == Py_None) return 0;
+  v = PyDict_GetItemWithError(resolved, idr);
+  if (!v) return PyErr_Occurred() ? -1 : 0;
+  if (!PyDict_CheckExact(v) || PyDict_GET_SIZE(v) == 0) return 0;
+  *nym = v;
+  return 1;
+}
+
+// phase A for one request: 0 = not the fast path (nothing appended, no
+// reference kept), 1 = *it filled and holding new references to idr, sig_o and
+// vk_o (taken before ser(), which may run Python code: str() of an int
+// subclass could otherwise drop the request's last reference to them), -1 = error.
+int collect_one(PyObject* req, PyObject* clients, PyObject* resolved, PyObject* excluded, Py_ssize_t k,
+                std::string& msgs, FastItem* it) {
   if (!PyDict_CheckExact(req)) return 0;
   PyObject* idr = PyDict_GetItem(req, g_k_identifier);
   PyObject* sig = PyDict_GetItem(req, g_k_signature);
   if (!idr || !sig) return 0;
   it->k = k;
-  it->idr = idr;
   if (!ascii_str(sig, &it->sig, &it->sig_n) || !ascii_str(idr, &it->idr_p, &it->idr_n) || it->sig_n == 0 ||
       it->idr_n == 0)
     return 0;
-  PyObject* nym = PyDict_GetItemWithError(clients, idr);
-  if (!nym) return PyErr_Occurred() ? -1 : 0;
-  if (!PyDict_CheckExact(nym) || PyDict_GET_SIZE(nym) == 0) return 0;
+  PyObject* nym = nullptr;
+  const int lr = lookup_nym(clients, resolved, idr, &nym);
+  if (lr <= 0) return lr;
   PyObject* verkey = PyDict_GetItem(nym, g_k_verkey);
   if (!verkey || !ascii_str(verkey, &it->vk_p, &it->vk_n)) return 0;
-  it->sig_o = sig;
-  it->vk_o = verkey;
   if (it->vk_n == 0) {
     it->vk_kind = 0;
   } else if (it->vk_p[0] == '~') {
@@ -609,10 +631,19 @@ int collect_one(PyObject* req, PyObject* clients, PyObject* excluded, Py_ssize_t
   } else {
     it->vk_kind = 2;
   }
+  Py_INCREF(idr);
+  Py_INCREF(sig);
+  Py_INCREF(verkey);
+  it->idr = idr;
+  it->sig_o = sig;
+  it->vk_o = verkey;
   const size_t mark = msgs.size();
   const int r = ser(req, 0, excluded, msgs);
   if (r != 1) {
     msgs.resize(mark);
+    Py_DECREF(idr);
+    Py_DECREF(sig);
+    Py_DECREF(verkey);
     return r;
   }
   return 1;
@@ -647,12 +678,17 @@ PyObject* py_last_phases(PyObject*, PyObject*) {
 }
 
 PyObject* py_auth_core_batch(PyObject*, PyObject* args) {
-  PyObject *reqs, *clients, *excluded;
+  PyObject *reqs, *clients, *excluded, *resolved = Py_None;
   unsigned long long vaddr;
   unsigned int mask;
   int threads;
-  if (!PyArg_ParseTuple(args, "OO!OKIi", &reqs, &PyDict_Type, &clients, &excluded, &vaddr, &mask, &threads))
+  if (!PyArg_ParseTuple(args, "OO!OKIi|O", &reqs, &PyDict_Type, &clients, &excluded, &vaddr, &mask, &threads,
+                        &resolved))
     return nullptr;
+  if (resolved != Py_None && !PyDict_Check(resolved)) {
+    PyErr_SetString(PyExc_TypeError, "resolved must be a dict or None");
+    return nullptr;
+  }
   const verify_fn_t verify = reinterpret_cast<verify_fn_t>(uintptr_t(vaddr));
   PyObject* seq = PySequence_Fast(reqs, "auth_core_batch needs a sequence of requests");
   if (!seq) return nullptr;
@@ -664,24 +700,21 @@ PyObject* py_auth_core_batch(PyObject*, PyObject* args) {
   std::vector<uint64_t> moff(1, 0);
   std::vector<Py_ssize_t> slow_idx;
   double t0 = now_s(), t1 = t0, t2 = t0;
-  // phase A
-  for (Py_ssize_t k = 0; k < n; k++) {
-    FastItem it;
-    const int r = collect_one(PySequence_Fast_GET_ITEM(seq, k), clients, excluded, k, msgs, &it);
-    if (r < 0) { Py_DECREF(seq); return nullptr; }
-    if (r == 0) { slow_idx.push_back(k); continue; }
-    Py_INCREF(it.idr);
-    Py_INCREF(it.sig_o);
-    Py_INCREF(it.vk_o);
-    items.push_back(it);
-    moff.push_back(uint64_t(msgs.size()));
-  }
-  struct Hold {  // drop the item references on every return path (GIL held)
+  struct Hold {  // drop the item references on every return path (GIL held), phase A's too
     std::vector<FastItem>& v;
     ~Hold() {
       for (FastItem& it : v) { Py_DECREF(it.idr); Py_DECREF(it.sig_o); Py_DECREF(it.vk_o); }
     }
   } hold{items};
+  // phase A
+  for (Py_ssize_t k = 0; k < n; k++) {
+    FastItem it;
+    const int r = collect_one(PySequence_Fast_GET_ITEM(seq, k), clients, resolved, excluded, k, msgs, &it);
+    if (r < 0) { Py_DECREF(seq); return nullptr; }
+    if (r == 0) { slow_idx.push_back(k); continue; }
+    items.push_back(it);
+    moff.push_back(uint64_t(msgs.size()));
+  }
   const size_t nf = items.size();
   const double ta = now_s();
   g_phase_s[0] = ta - t0;

@@ -327,6 +327,14 @@ class DeviceBuffer:
         _check(lib().edv_d2h(self.device, out.ctypes.data, self.ptr, nbytes))
         return out.view(dtype)
 
+    def download_at(self, offset, nbytes, dtype=np.uint8):
+        """Bytes [offset, offset + nbytes) of the buffer."""
+        assert 0 <= offset and offset + nbytes <= self.nbytes
+        out = np.empty(nbytes, dtype=np.uint8)
+        if nbytes:
+            _check(lib().edv_d2h(self.device, out.ctypes.data, self.ptr + offset, nbytes))
+        return out.view(dtype)
+
     def free(self):
         if self.ptr:
             lib().edv_dev_free(self.device, self.ptr)

@@ -318,12 +318,27 @@ class Pool:
         while min(nd.ordered for nd in self.nodes.values()) < expect:
             work = sum(nd.prod(self) for nd in self.nodes.values())
             idle = 0 if work else idle + 1
-        if self.executor is not None:
-            self.executor.shutdown(wait=True)
             if idle > max_idle_rounds:
+                self.drain()
                 raise RuntimeError("pool stalled: ordered %s of %d" % ([nd.ordered for nd in self.nodes.values()],
                                                                       expect))
+        self.drain()
         return time.perf_counter() - t0
+
+    def drain(self):
+        """Overlap mode: handle every batch still in flight (its verdicts are
+        applied as the node's next prod would), so no future outlives run()."""
+        for nd in self.nodes.values():
+            pend, nd._pending = nd._pending, None
+            if pend is not None:
+                nd._finish(*pend)
+
+    def close(self):
+        """Stop the overlap mode's background thread (the pool is unusable after)."""
+        self.drain()
+        if self.executor is not None:
+            self.executor.shutdown(wait=True)
+            self.executor = None
 
     def stats(self, wall_s, n_reqs):
         nodes = list(self.nodes.values())

@@ -10,6 +10,7 @@ order; each batch-capable one (authenticate_batch) sees all requests still
 alive at its position in one call, i.e. one GPU launch per authenticator.
 """
 import gc
+import threading
 from contextlib import contextmanager
 from copy import deepcopy
 from typing import Optional
@@ -19,19 +20,33 @@ from .constants import OPERATION, TXN_TYPE
 from .exceptions import NoAuthenticatorFound
 
 
+_gc_lock = threading.Lock()
+_gc_depth = 0       # paused sections in progress, over all threads
+_gc_was = False     # GC state when the first of them began
+
+
 @contextmanager
 def gc_paused():
     """Pause the cyclic GC while a batch makes one small container per request
     (identifier sets, lists): at node scale the allocations otherwise trigger
     repeated collections over every live object; the young objects are
-    collected once, after.  Re-entrant; restores the previous state."""
-    was = gc.isenabled()
-    gc.disable()
+    collected once, after.  The GC flag is process-global and batches may run
+    on several threads at once (the pool's overlap mode), so the pause is
+    counted under a lock: the first section to begin records the state, the
+    last one to end restores it."""
+    global _gc_depth, _gc_was
+    with _gc_lock:
+        if _gc_depth == 0:
+            _gc_was = gc.isenabled()
+            gc.disable()
+        _gc_depth += 1
     try:
         yield
     finally:
-        if was:
-            gc.enable()
+        with _gc_lock:
+            _gc_depth -= 1
+            if _gc_depth == 0 and _gc_was:
+                gc.enable()
 
 
 class ReqAuthenticator:

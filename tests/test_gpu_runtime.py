@@ -321,14 +321,48 @@ def test_multi_device_path_on_virtual_devices():
     assert out["bad_mask"] == "EdvUnavailable"
 
 
+def _bench(args, env=None, launcher=None, timeout=420):
+    cmd = (launcher or [sys.executable]) + [os.path.join(ROOT, "bench.py")] + args
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]           # exactly one JSON line on stdout
+    return json.loads(lines[0])
+
+
+_QUICK = ["--steps", "2", "--reps", "2", "--warmup", "1", "--warmup-seconds", "0", "--no-cpu-baseline"]
+
+
 def test_bench_c3_mode_bounded():
     """bench.py --total (C3 split by request index, 5 % damaged at known
-    positions, accept bytes checked) on a bounded total."""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--total", "524288", "--steps", "2",
-                        "--reps", "2", "--warmup", "1", "--warmup-seconds", "0", "--no-cpu-baseline"],
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
-    line = json.loads(r.stdout.strip().splitlines()[-1])
+    positions over four kinds, accept bytes checked) on a bounded total."""
+    line = _bench(["--total", "524288"] + _QUICK)
     assert line["verdicts_as_expected"] is True
     assert line["config"]["workload"].startswith("C3")
-    assert line["value"] > 1e6
+    assert line["n_gpus"] == 1 and line["value"] > 1e6
+
+
+def test_bench_two_gpus_launched_by_bench():
+    """python bench.py --gpus 2 (no launcher around it) on two logical devices
+    (EDV_VIRTUAL_DEVICES=2 on this one-GPU box): bench starts one process per
+    device, C3 is the default for N > 1, every shard's accept bytes come back
+    into their slice of the host array and match the construction."""
+    env = dict(os.environ, EDV_VIRTUAL_DEVICES="2")
+    env.pop("WORLD_SIZE", None)
+    line = _bench(["--gpus", "2", "--total", "1048576"] + _QUICK, env=env)
+    assert line["n_gpus"] == 2 and line["verdicts_as_expected"] is True
+    assert line["config"]["workload"].startswith("C3") and line["config"]["per_gpu"] == 524288
+    assert line["timing"]["launch"] == "ranks started by bench.py"
+
+
+def test_bench_two_gpus_under_torch_distributed_run():
+    """The driver's N > 1 form: python -m torch.distributed.run --nproc-per-node 2
+    bench.py --gpus 2 (ranks from the environment, device = LOCAL_RANK; the
+    ranks themselves import no torch)."""
+    env = dict(os.environ, EDV_VIRTUAL_DEVICES="2")
+    env.pop("WORLD_SIZE", None)
+    launcher = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000)]
+    line = _bench(["--gpus", "2", "--total", "1048576"] + _QUICK, env=env, launcher=launcher)
+    assert line["n_gpus"] == 2 and line["verdicts_as_expected"] is True
+    assert line["timing"]["launch"] == "torch.distributed.run ranks"

@@ -308,3 +308,89 @@ def test_native_request_digests_equal_request_get_digest(monkeypatch):
     monkeypatch.setattr(edv, "sha256_address", lambda: addr)
     monkeypatch.setattr(edv, "sha256_batch", cpu_sha256_batch)
     assert digest.request_digests(reqs) == want
+
+
+class _RecordingState:
+    """The reference state's get(key, isCommitted) contract; records every read."""
+
+    def __init__(self):
+        self.kv, self.reads = {}, []
+
+    def get(self, key, isCommitted=True):
+        self.reads.append(isCommitted)
+        return self.kv.get(key)
+
+
+@pytest.mark.parametrize("n_keys_on_device", [10**9, 1])
+def test_whole_batch_native_path_with_state_verkeys(monkeypatch, n_keys_on_device):
+    """SimpleAuthNr.getVerkey's second source (client_authn.py:148-160 ->
+    domain_req_handler.py:158-167: the NYM under sha256(identifier) in the
+    uncommitted state) on the whole-batch native path: identifiers known only
+    to the state stay native (one verify call for them and the clients-map
+    ones), and every outcome equals the sequential reference chain, including
+    state values that are absent, empty, not JSON or not an object, and a
+    clients entry that is empty (which falls through to the state)."""
+    import json
+    import hashlib
+    import test_authn_host as H
+    from indy_plenum_amd import client_authn, digest
+    from indy_plenum_amd.client_authn import CoreAuthNr, nym_to_state_key
+    r = random.Random(77)
+    signers = [H.Signer(seed=bytes([k + 1, 7]) * 16) for k in range(10)]
+    for k, s in enumerate(signers):
+        if k % 3 == 1:            # abbreviated verkeys
+            s.identifier = base58.b58encode(s.pk[:16]).decode()
+    st = _RecordingState()
+    auth = CoreAuthNr(state=st)
+    for s in signers[:3]:
+        auth.addIdr(s.identifier, s.verkey)
+    for k, s in enumerate(signers[3:8]):
+        vk = "~" + base58.b58encode(s.pk[16:]).decode() if s.identifier != s.verkey else s.verkey
+        st.kv[nym_to_state_key(s.identifier)] = json.dumps({"verkey": vk, "role": None}).encode()
+    auth.clients[signers[3].identifier] = {}          # falsy clients entry: the state decides
+    odd = ["NotJson1", "ListNym1", "EmptyNym", "NoVerkey", "Absent99"]
+    st.kv[nym_to_state_key("NotJson1")] = b"{not json"
+    st.kv[nym_to_state_key("ListNym1")] = b"[1, 2]"
+    st.kv[nym_to_state_key("EmptyNym")] = b"{}"
+    st.kv[nym_to_state_key("NoVerkey")] = b'{"role": "0"}'
+    reqs = []
+    for i in range(600):
+        s = r.choice(signers[:8])
+        req = {"identifier": s.identifier, "reqId": i, "operation": {"type": "1", "n": i}, "protocolVersion": 2}
+        kind = r.randrange(10)
+        if kind == 0:
+            req["identifier"] = r.choice(odd)
+        if kind == 1:
+            req["signature"] = s.sign({**req, "reqId": -1})
+        else:
+            req["signature"] = s.sign(req)
+        reqs.append(req)
+    with monkeypatch.context() as m:
+        m.setattr(edv, "open_batch", H.oracle_open_batch)
+        want = [H.outcome(lambda q=q: auth.authenticate(dict(q))) for q in reqs]
+    assert st.reads and not any(st.reads)             # every state read is uncommitted
+    calls = []
+    cb, addr = _oracle_verify_callback(calls)
+    monkeypatch.setattr(edv, "verify_address", lambda: addr)
+    monkeypatch.setattr(client_authn.CoreAuthMixin, "STATE_KEYS_ON_DEVICE", n_keys_on_device)
+    monkeypatch.setattr(digest, "nym_state_keys", lambda nyms, device_mask=0:
+                        [hashlib.sha256(x.encode()).digest() for x in nyms])
+    slow_calls = []
+
+    def counting_open(items, device_mask=0):
+        items = list(items)
+        slow_calls.append(len(items))
+        return H.oracle_open_batch(items)
+    monkeypatch.setattr(edv, "_OPEN_BATCH", counting_open)
+    monkeypatch.setattr(edv, "open_batch", counting_open)
+    st.reads.clear()
+    got = auth.authenticate_batch(reqs)
+    got = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in got]
+    assert got == want
+    assert not any(st.reads)
+    n_odd = sum(1 for q in reqs if q["identifier"] in odd)
+    # every request with a resolvable verkey went native, state-only identifiers included
+    assert len(calls) == 1 and calls[0] == len(reqs) - n_odd
+    assert sum(slow_calls) == 0                       # the odd ones fail before any verify
+    assert {o[1] for o in got if o[0] == "raise"} >= {"UnknownIdentifier", "CouldNotAuthenticate",
+                                                      "InsufficientCorrectSignatures"}

@@ -60,7 +60,10 @@ def test_pool_orders_every_valid_request_once(batched, overlap, monkeypatch):
     pool = Pool(factory(signers), n=4, batched=batched, digest_fn=cpu_digests, overlap=overlap, client_quota=16,
                 max_batch=7)
     pool.submit(reqs)
-    wall = pool.run(len(valid))
+    try:
+        wall = pool.run(len(valid))
+    finally:
+        pool.close()
     st = pool.stats(wall, len(valid))
     assert st["ordered_per_node"] == [len(valid)] * 4
     assert st["nacks_per_node"] == [len(reqs) - len(valid)] * 4
@@ -71,3 +74,21 @@ def test_pool_orders_every_valid_request_once(batched, overlap, monkeypatch):
     assert st["verifies"] == 4 * len(reqs) + 4 * 3 * len(valid)
     if batched:
         assert st["auth_calls"] < st["verifies"] / 4   # one authenticate_batch per prod
+
+
+@pytest.mark.parametrize("batched,overlap", [(False, False), (True, False), (True, True)])
+def test_pool_stall_raises(batched, overlap, monkeypatch):
+    """A pool asked to order more requests than it was given stops with
+    RuntimeError after max_idle_rounds idle rounds instead of spinning."""
+    monkeypatch.setattr(edv, "open_batch", lambda items, device_mask=0: H.oracle_open_batch(list(items)))
+    signers, reqs, valid = flood(n_valid=12, n_bad_sig=3, n_unknown=1, seed=9)
+    pool = Pool(factory(signers), n=4, batched=batched, digest_fn=cpu_digests, overlap=overlap, client_quota=16)
+    pool.submit(reqs)
+    try:
+        with pytest.raises(RuntimeError, match="stalled"):
+            pool.run(len(valid) + 1, max_idle_rounds=5)
+        # nothing is left in flight and every valid request was still ordered once
+        assert all(nd._pending is None for nd in pool.nodes.values())
+        assert [nd.ordered for nd in pool.nodes.values()] == [len(valid)] * 4
+    finally:
+        pool.close()

@@ -23,7 +23,10 @@ def _run(signers, reqs, valid, batched, digest_fn, overlap=False):
     pool = Pool(factory(signers), n=4, batched=batched, digest_fn=digest_fn, overlap=overlap, client_quota=50,
                 max_batch=40)
     pool.submit(reqs)
-    wall = pool.run(len(valid))
+    try:
+        wall = pool.run(len(valid))
+    finally:
+        pool.close()
     st = pool.stats(wall, len(valid))
     st["ordered_keys"] = [sorted(nd.ordered_keys) for nd in pool.nodes.values()]
     return st

@@ -5,9 +5,10 @@
   (indy-plenum_amd/shard.py) and against the properties SURVEY.md section 8e
   asks for: contiguous, covering, equal counts for one message length, equal
   estimated cost (sum of 40 + SHA-512 blocks) for C4's 200 B - 4 KB lengths.
-* A world_size-2 torch.distributed (gloo) run of the shard + accept all-gather
-  logic bench.py uses with RCCL on the GPU box; each rank verifies its shard
-  with the checker (this tests the sharding, not the kernels).
+* A world_size-2 torch.distributed (gloo) run of the shard split and the
+  gather of per-shard accept bytes into request order; each rank verifies its
+  shard with the checker (this tests the sharding, not the kernels).  bench.py's
+  own rank rendezvous (no torch) is tested in tests/test_bench_cpu.py.
 """
 import os
 import socket
@@ -33,10 +34,8 @@ def _worker(rank, world, port, q):
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
     sys.path.insert(0, os.path.dirname(here))
-    sys.path.insert(0, os.path.join(os.path.dirname(here), "tools"))
     import torch.distributed as dist
     import oracle_lib as orc
-    from dist_gather import gather_accept
     from indy_plenum_amd import shard
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -47,7 +46,11 @@ def _worker(rank, world, port, q):
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         s, p, m, o = shard.slice_batch(sigs, pks, msgs, off, lo, hi)
         local = np.frombuffer(orc.verify_batch(s.tobytes(), p.tobytes(), m.tobytes(), o, hi - lo, 2), np.uint8)
-        full = gather_accept(dist, local, bounds)
+        parts = [None] * world
+        dist.all_gather_object(parts, local.tobytes())
+        full = np.zeros(N, np.uint8)
+        for r, p in enumerate(parts):
+            full[int(bounds[r]):int(bounds[r + 1])] = np.frombuffer(p, np.uint8)
         if rank == 0:
             whole = np.frombuffer(orc.verify_batch(sigs.tobytes(), pks.tobytes(), msgs.tobytes(), off, N, 4),
                                   np.uint8)

@@ -73,6 +73,8 @@ def summarise(root):
             d["gpu_busy_cycles"] = busy
             # fraction of all SIMD cycles in which a VALU instruction was issuing (quad-cycle units)
             d["valu_busy"] = 4.0 * avg["SQ_ACTIVE_INST_VALU"] / (busy * N_SIMD)
+        if avg.get("TCC_HIT_sum", 0.0) + avg.get("TCC_MISS_sum", 0.0) > 0:
+            d["l2_hit_rate"] = avg["TCC_HIT_sum"] / (avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
         if "SQ_WAVE_CYCLES" in avg:
             wc = avg["SQ_WAVE_CYCLES"]
             d["wave_cycle_split"] = {c: avg.get(c, 0.0) / wc for c in
