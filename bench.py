@@ -594,9 +594,11 @@ def c5_leg(n=20000, n_cpu=2000):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_pool
     out = bench_pool.c5(n, n_cpu)
-    g = out["gpu_batched"]
+    g = out["gpu_batched_overlap"]
     out["summary"] = {"gpu_ordered_req_per_s": g["ordered_req_per_s_one_process"],
                       "gpu_auth_share_of_node_time": g["auth_share_of_node_time"],
+                      "gpu_vs_no_verify_ceiling": out["overlap_vs_ceiling"],
+                      "gpu_mode": "overlap: authenticate_batch_submit per prod, handed over at the next prod",
                       "cpu_ordered_req_per_s": out.get("cpu_reference", {}).get("ordered_req_per_s_one_process"),
                       "cpu_auth_share_of_node_time": out.get("cpu_reference", {}).get("auth_share_of_node_time")}
     return out

@@ -68,12 +68,12 @@ int edv_verify_batch(const uint8_t *sigs, const uint8_t *pks, const uint8_t *msg
  * Asynchronous form of edv_verify_batch on one device (the batched call site of
  * plenum/server/client_authn.py:92-112 when the Node verifies one batch per prod
  * and keeps going): queues the H2D copies, the kernels and the D2H of the
- * verdicts and returns a ticket at once.  Batches alternate between two slots,
+ * verdicts and returns a ticket at once.  Batches take eight slots in turn,
  * so batch k+1's copies (and, for pageable inputs, its staging memcpy, done in
  * this call) run while batch k computes: back to back, the host path then runs
  * at the kernels' rate rather than copy + kernels.  The caller's buffers must
  * stay valid and unchanged, and `accept` unread, until edv_wait_async(device,
- * ticket) returns 0; a submission waits for the batch two submissions back
+ * ticket) returns 0; a submission waits for the batch eight submissions back
  * (completing it as edv_wait_async would) before reusing its slot.  Same
  * verdicts, arguments and alignment rules as edv_verify_batch.
  */
@@ -82,6 +82,19 @@ int edv_verify_batch_async(const uint8_t *sigs, const uint8_t *pks, const uint8_
 /* Wait for batch `ticket` of `device` and hand over its verdicts (0 at once if
  * it already was); EDV_E_ARG for a ticket never issued. */
 int edv_wait_async(int device, int64_t ticket);
+/*
+ * edv_verify_batch_async that also returns, when `digests` is not NULL, the
+ * SHA-256 of every message (digests: n x 32 bytes, same lifetime rules as
+ * `accept`), computed on the device from the bytes already copied for the
+ * verify.  For a request whose signing bytes are its signingState's
+ * serialization these are Request.getDigest (plenum/common/request.py:71-72),
+ * which the Node computes per request next to the signature check
+ * (plenum/server/node.py:2093-2147); the caller decides which requests that
+ * holds for.  Ticket and wait as for edv_verify_batch_async.
+ */
+int edv_verify_digest_batch_async(const uint8_t *sigs, const uint8_t *pks, const uint8_t *msgs,
+                                  const uint64_t *msg_off, uint64_t n, uint8_t *accept, uint8_t *digests, int device,
+                                  int64_t *ticket);
 
 /*
  * Same verdicts for inputs already resident in device memory of `device`;

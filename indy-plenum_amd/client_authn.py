@@ -59,6 +59,31 @@ class ClientAuthNr:
         """The verification key for an identifier."""
 
 
+class PendingAuth:
+    """A batch whose verdicts (and optional request digests) are still on the
+    way: result() -> the per-request list authenticate_batch returns;
+    digests() -> per request the Request.getDigest hex string or None.  The
+    first call waits; both may be called any number of times."""
+
+    __slots__ = ("_finish", "_res")
+
+    def __init__(self, finish):
+        self._finish = finish
+        self._res = None
+
+    def _get(self):
+        if self._res is None:
+            self._res = self._finish()
+            self._finish = None
+        return self._res
+
+    def result(self):
+        return self._get()[0]
+
+    def digests(self):
+        return self._get()[1]
+
+
 class _Raise:
     """A recorded exception: raised at replay time only if the sequential loop reaches it."""
 
@@ -360,6 +385,33 @@ class CoreAuthMixin:
             return None
         return _edvhost.auth_core_batch(reqs, self.clients, self.excluded_from_signing, edv.verify_address(),
                                         edv.BATCH_DEVICE_MASK, edv.PREP_THREADS, self._state_nyms(reqs))
+
+    def authenticate_batch_submit(self, reqs, verifier: Verifier = DidVerifier, digests: bool = False):
+        """Asynchronous authenticate_batch: host prep now and the device call
+        queued (edv_verify_digest_batch_async), so the caller keeps working while
+        the GPU verifies; PendingAuth.result() waits and returns what
+        authenticate_batch returns.  digests=True also asks the device for
+        Request.getDigest (request.py:71-72) of every request whose signing bytes
+        are its signingState serialization (PendingAuth.digests(); None entries
+        for the rest).  Without the stock native path the work is done here, at
+        once, and the PendingAuth only hands it over."""
+        if self._stock(verifier) and edv.native_batch_enabled():
+            submit, wait = edv.async_addresses()
+            h = _edvhost.auth_core_submit(reqs, self.clients, self.excluded_from_signing, submit, wait,
+                                          edv.BATCH_DEVICE, edv.PREP_THREADS, self._state_nyms(reqs), digests)
+            return PendingAuth(lambda: self._finish_native(reqs, h, verifier))
+        out = self.authenticate_batch(reqs, verifier)
+        return PendingAuth(lambda: (out, [None] * len(reqs)))
+
+    def _finish_native(self, reqs, handle, verifier):
+        out, slow, rejected, digs = _edvhost.auth_core_finish(handle)
+        for k in rejected:
+            out[k] = InsufficientCorrectSignatures(0, 1)
+        if slow:
+            sub = [reqs[k] for k in slow]
+            for k, r in zip(slow, self._batch_planned(sub, [None] * len(sub), verifier)):
+                out[k] = r
+        return out, (digs if digs is not None else [None] * len(reqs))
 
     # below this many state keys hashlib beats a device round trip
     STATE_KEYS_ON_DEVICE = 512

@@ -583,6 +583,7 @@ inline bool ascii_str(PyObject* o, const uint8_t** p, size_t* n) {
 
 // phase A for one request: false = not the fast path (nothing appended)
 PyObject *g_k_identifier, *g_k_signature, *g_k_verkey;  // interned key strings (module init)
+PyObject *g_k_reqid, *g_k_operation, *g_k_protocol;
 
 // verkey source of one identifier, as SimpleAuthNr.getVerkey (client_authn.py:148-160)
 // reads it: the in-memory `clients` entry unless it is falsy, else the NYM the
@@ -677,119 +678,170 @@ PyObject* py_last_phases(PyObject*, PyObject*) {
                        "verify_s", g_phase_s[2], "output_s", g_phase_s[3]);
 }
 
-PyObject* py_auth_core_batch(PyObject*, PyObject* args) {
-  PyObject *reqs, *clients, *excluded, *resolved = Py_None;
-  unsigned long long vaddr;
-  unsigned int mask;
-  int threads;
-  if (!PyArg_ParseTuple(args, "OO!OKIi|O", &reqs, &PyDict_Type, &clients, &excluded, &vaddr, &mask, &threads,
-                        &resolved))
-    return nullptr;
-  if (resolved != Py_None && !PyDict_Check(resolved)) {
-    PyErr_SetString(PyExc_TypeError, "resolved must be a dict or None");
-    return nullptr;
-  }
-  const verify_fn_t verify = reinterpret_cast<verify_fn_t>(uintptr_t(vaddr));
-  PyObject* seq = PySequence_Fast(reqs, "auth_core_batch needs a sequence of requests");
-  if (!seq) return nullptr;
-  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
-  PyObject *out = nullptr, *slow = nullptr, *rejected = nullptr, *res = nullptr;
+// The state of one whole-batch call between its phases (GIL held except where
+// noted).  The item references and the arena are released by the destructor.
+typedef int (*submit_fn_t)(const uint8_t*, const uint8_t*, const uint8_t*, const uint64_t*, uint64_t, uint8_t*,
+                           uint8_t*, int, int64_t*);
+typedef int (*wait_fn_t)(int, int64_t);
+PyObject *g_k_signatures, *g_k_fees;
+
+struct Batch {
   std::vector<FastItem> items;
-  items.reserve(size_t(n));
-  std::string msgs;
-  std::vector<uint64_t> moff(1, 0);
   std::vector<Py_ssize_t> slow_idx;
-  double t0 = now_s(), t1 = t0, t2 = t0;
-  struct Hold {  // drop the item references on every return path (GIL held), phase A's too
-    std::vector<FastItem>& v;
-    ~Hold() {
-      for (FastItem& it : v) { Py_DECREF(it.idr); Py_DECREF(it.sig_o); Py_DECREF(it.vk_o); }
+  std::vector<uint8_t> good, dig_ok;  // per fast item: decoded; digest == sha256(signing bytes)
+  std::string msgs;
+  std::vector<uint64_t> moff = std::vector<uint64_t>(1, 0);
+  Arena* ar = nullptr;
+  size_t o_pk = 0, o_off = 0, o_msg = 0, o_acc = 0, o_dig = 0;
+  Py_ssize_t n = 0;
+  bool want_dig = false;
+  // asynchronous submission (auth_core_submit): the batch is in flight until waited for
+  bool pending = false;
+  int device = 0;
+  int64_t ticket = -1;
+  wait_fn_t wait = nullptr;
+  ~Batch() {
+    for (FastItem& it : items) { Py_DECREF(it.idr); Py_DECREF(it.sig_o); Py_DECREF(it.vk_o); }
+    if (ar) g_arenas.push_back(ar);
+  }
+};
+
+// Request.getDigest (request.py:71-72) hashes the serialization of signingState =
+// {identifier, reqId, operation[, protocolVersion if not None]} (request.py:77-87);
+// the signing bytes serialize the request without signature / signatures / fees
+// (client_authn.py:174, :222-223).  The two are the same bytes exactly when the
+// request's other keys are identifier, reqId, operation and, unless it is None,
+// protocolVersion.  -1 = error.
+int digest_is_signing_bytes(PyObject* req) {
+  Py_ssize_t pos = 0;
+  PyObject *k, *v;
+  int have = 0;
+  while (PyDict_Next(req, &pos, &k, &v)) {
+    if (!PyUnicode_CheckExact(k)) return 0;
+    if (k == g_k_signature || k == g_k_signatures || k == g_k_fees) continue;
+    if (k == g_k_identifier || k == g_k_operation || k == g_k_reqid) { have++; continue; }
+    if (k == g_k_protocol) {
+      if (v == Py_None) return 0;
+      continue;
     }
-  } hold{items};
-  // phase A
-  for (Py_ssize_t k = 0; k < n; k++) {
+    // a key equal to one of ours but not the interned object: compare by value
+    for (PyObject* kk : {g_k_signature, g_k_signatures, g_k_fees, g_k_identifier, g_k_operation, g_k_reqid,
+                         g_k_protocol}) {
+      const int eq = PyUnicode_Compare(k, kk);
+      if (eq == -1 && PyErr_Occurred()) return -1;
+      if (eq == 0) return 0;  // unusual key object: leave it to the general digest path
+    }
+    return 0;
+  }
+  return have == 3 ? 1 : 0;
+}
+
+// phase A: collect, look verkeys up, serialize (GIL held)
+int collect_all(Batch& b, PyObject* seq, PyObject* clients, PyObject* resolved, PyObject* excluded) {
+  b.n = PySequence_Fast_GET_SIZE(seq);
+  b.items.reserve(size_t(b.n));
+  for (Py_ssize_t k = 0; k < b.n; k++) {
+    PyObject* req = PySequence_Fast_GET_ITEM(seq, k);
     FastItem it;
-    const int r = collect_one(PySequence_Fast_GET_ITEM(seq, k), clients, resolved, excluded, k, msgs, &it);
-    if (r < 0) { Py_DECREF(seq); return nullptr; }
-    if (r == 0) { slow_idx.push_back(k); continue; }
-    items.push_back(it);
-    moff.push_back(uint64_t(msgs.size()));
+    const int r = collect_one(req, clients, resolved, excluded, k, b.msgs, &it);
+    if (r < 0) return -1;
+    if (r == 0) { b.slow_idx.push_back(k); continue; }
+    b.items.push_back(it);
+    b.moff.push_back(uint64_t(b.msgs.size()));
+    if (b.want_dig) {
+      const int d = digest_is_signing_bytes(req);
+      if (d < 0) return -1;
+      b.dig_ok.push_back(uint8_t(d));
+    }
   }
-  const size_t nf = items.size();
-  const double ta = now_s();
-  g_phase_s[0] = ta - t0;
-  t0 = t1 = t2 = ta;
-  std::vector<uint8_t> good(nf, 1);
-  Arena* ar = take_arena();
-  // arena layout: sigs 64 nf | pks 32 nf | off 8 (nf + 1) | msgs (+64 slack) | accept nf
-  const size_t o_pk = 64 * nf, o_off = o_pk + 32 * nf, o_msg = o_off + 8 * (nf + 1),
-               o_acc = o_msg + ((msgs.size() + 64 + 63) / 64) * 64;
-  int rc = 0;
-  if (nf && !ar->ensure(o_acc + nf)) {
-    g_arenas.push_back(ar);
-    Py_DECREF(seq);
-    return PyErr_NoMemory();
+  return 0;
+}
+
+// phase B: arena + base58 decoding on `threads` threads (releases the GIL)
+int pack_all(Batch& b, int threads) {
+  const size_t nf = b.items.size();
+  b.good.assign(nf, 1);
+  if (!nf) return 0;
+  b.ar = take_arena();
+  // arena layout: sigs 64 nf | pks 32 nf | off 8 (nf + 1) | msgs (+64 slack) | accept nf | digests 32 nf
+  b.o_pk = 64 * nf;
+  b.o_off = b.o_pk + 32 * nf;
+  b.o_msg = b.o_off + 8 * (nf + 1);
+  b.o_acc = b.o_msg + ((b.msgs.size() + 64 + 63) / 64) * 64;
+  b.o_dig = b.o_acc + ((nf + 63) / 64) * 64;
+  if (!b.ar->ensure(b.o_dig + (b.want_dig ? 32 * nf : 0))) {
+    PyErr_NoMemory();
+    return -1;
   }
-  if (nf) {
-    uint8_t* base = ar->p;
-    Py_BEGIN_ALLOW_THREADS
-    // phase B: decode on T threads; the message bytes and offsets are copied beside
-    const int T = nf < 2048 ? 1 : std::max(1, std::min(threads, 32));
-    auto part = [&](int t) {
-      const size_t lo = nf * size_t(t) / size_t(T), hi = nf * size_t(t + 1) / size_t(T);
-      for (size_t i = lo; i < hi; i++)
-        if (!decode_one(items[i], base + 64 * i, base + o_pk + 32 * i)) {
-          good[i] = 0;
-          memset(base + 64 * i, 0, 64);  // verified for nothing; the verdict is ignored
-          memset(base + o_pk + 32 * i, 0, 32);
-        }
-      const size_t mlo = msgs.size() * size_t(t) / size_t(T), mhi = msgs.size() * size_t(t + 1) / size_t(T);
-      memcpy(base + o_msg + mlo, msgs.data() + mlo, mhi - mlo);
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; t++) th.emplace_back(part, t);
-    part(0);
-    for (auto& x : th) x.join();
-    memcpy(base + o_off, moff.data(), 8 * (nf + 1));
-    memset(base + o_msg + msgs.size(), 0, 64);
-    t1 = now_s();
-    // phase C: one device call
-    rc = verify(base, base + o_pk, base + o_msg, reinterpret_cast<const uint64_t*>(base + o_off), uint64_t(nf),
-                base + o_acc, mask);
-    t2 = now_s();
-    Py_END_ALLOW_THREADS
-  }
-  if (rc != 0) {
-    g_arenas.push_back(ar);
-    Py_DECREF(seq);
-    PyErr_Format(PyExc_RuntimeError, "edv_verify_batch failed (%d)", rc);
-    return nullptr;
-  }
-  // phase D.  The cyclic GC is paused while the per-request lists are made:
-  // tens of thousands of new containers would otherwise trigger repeated
-  // collections that walk every live object of the node (30 ms per 64k batch,
-  // measured); the young objects are collected once, after.
+  uint8_t* base = b.ar->p;
+  Py_BEGIN_ALLOW_THREADS
+  const int T = nf < 2048 ? 1 : std::max(1, std::min(threads, 32));
+  auto part = [&](int t) {
+    const size_t lo = nf * size_t(t) / size_t(T), hi = nf * size_t(t + 1) / size_t(T);
+    for (size_t i = lo; i < hi; i++)
+      if (!decode_one(b.items[i], base + 64 * i, base + b.o_pk + 32 * i)) {
+        b.good[i] = 0;
+        memset(base + 64 * i, 0, 64);  // verified for nothing; the verdict is ignored
+        memset(base + b.o_pk + 32 * i, 0, 32);
+      }
+    const size_t mlo = b.msgs.size() * size_t(t) / size_t(T), mhi = b.msgs.size() * size_t(t + 1) / size_t(T);
+    memcpy(base + b.o_msg + mlo, b.msgs.data() + mlo, mhi - mlo);
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back(part, t);
+  part(0);
+  for (auto& x : th) x.join();
+  memcpy(base + b.o_off, b.moff.data(), 8 * (nf + 1));
+  memset(base + b.o_msg + b.msgs.size(), 0, 64);
+  Py_END_ALLOW_THREADS
+  return 0;
+}
+
+// phase D: (out, slow, rejected[, digests]).  The cyclic GC is paused while the
+// per-request lists are made: tens of thousands of new containers would
+// otherwise trigger repeated collections that walk every live object of the
+// node (30 ms per 64k batch, measured); the young objects are collected once, after.
+PyObject* build_output(Batch& b, bool with_digests) {
+  const size_t nf = b.items.size();
+  const uint8_t* acc = nf ? b.ar->p + b.o_acc : nullptr;
   const int gc_was = PyGC_Disable();
-  out = PyList_New(n);
-  slow = PyList_New(0);
-  rejected = PyList_New(0);
-  if (!out || !slow || !rejected) goto fail;
-  for (Py_ssize_t k = 0; k < n; k++) {
+  PyObject *out = PyList_New(b.n), *slow = PyList_New(0), *rejected = PyList_New(0), *digs = nullptr, *res = nullptr;
+  if (with_digests) digs = PyList_New(b.n);
+  if (!out || !slow || !rejected || (with_digests && !digs)) goto fail;
+  for (Py_ssize_t k = 0; k < b.n; k++) {
     Py_INCREF(Py_None);
     PyList_SET_ITEM(out, k, Py_None);
+    if (digs) {
+      Py_INCREF(Py_None);
+      PyList_SET_ITEM(digs, k, Py_None);
+    }
   }
-  for (Py_ssize_t k : slow_idx) {
+  for (Py_ssize_t k : b.slow_idx) {
     PyObject* v = PyLong_FromSsize_t(k);
     if (!v || PyList_Append(slow, v) < 0) { Py_XDECREF(v); goto fail; }
     Py_DECREF(v);
   }
   for (size_t i = 0; i < nf; i++) {
-    const FastItem& it = items[i];
-    if (!good[i]) {
+    const FastItem& it = b.items[i];
+    if (digs && b.dig_ok[i]) {
+      static const char hexd[] = "0123456789abcdef";
+      const uint8_t* d = b.ar->p + b.o_dig + 32 * i;
+      char h[64];
+      for (int q = 0; q < 32; q++) {
+        h[2 * q] = hexd[d[q] >> 4];
+        h[2 * q + 1] = hexd[d[q] & 15];
+      }
+      PyObject* v = PyUnicode_FromStringAndSize(h, 64);
+      if (!v) goto fail;
+      PyObject* old = PyList_GET_ITEM(digs, it.k);
+      PyList_SET_ITEM(digs, it.k, v);
+      Py_DECREF(old);
+    }
+    if (!b.good[i]) {
       PyObject* v = PyLong_FromSsize_t(it.k);
       if (!v || PyList_Append(slow, v) < 0) { Py_XDECREF(v); goto fail; }
       Py_DECREF(v);
-    } else if (ar->p[o_acc + i]) {
+    } else if (acc[i]) {
       PyObject* l = PyList_New(1);
       if (!l) goto fail;
       Py_INCREF(it.idr);
@@ -804,22 +856,146 @@ PyObject* py_auth_core_batch(PyObject*, PyObject* args) {
     }
   }
   if (PyList_Sort(slow) < 0) goto fail;
-  g_phase_s[1] = t1 - t0;
-  g_phase_s[2] = t2 - t1;
-  g_phase_s[3] = now_s() - t2;
-  res = Py_BuildValue("(NNN)", out, slow, rejected);
+  res = with_digests ? Py_BuildValue("(NNNN)", out, slow, rejected, digs) : Py_BuildValue("(NNN)", out, slow, rejected);
   if (gc_was) PyGC_Enable();
-  g_arenas.push_back(ar);
-  Py_DECREF(seq);
   return res;
 fail:
   if (gc_was) PyGC_Enable();
   Py_XDECREF(out);
   Py_XDECREF(slow);
   Py_XDECREF(rejected);
-  g_arenas.push_back(ar);
-  Py_DECREF(seq);
+  Py_XDECREF(digs);
   return nullptr;
+}
+
+bool parse_resolved(PyObject* resolved) {
+  if (resolved != Py_None && !PyDict_Check(resolved)) {
+    PyErr_SetString(PyExc_TypeError, "resolved must be a dict or None");
+    return false;
+  }
+  return true;
+}
+
+PyObject* py_auth_core_batch(PyObject*, PyObject* args) {
+  PyObject *reqs, *clients, *excluded, *resolved = Py_None;
+  unsigned long long vaddr;
+  unsigned int mask;
+  int threads;
+  if (!PyArg_ParseTuple(args, "OO!OKIi|O", &reqs, &PyDict_Type, &clients, &excluded, &vaddr, &mask, &threads,
+                        &resolved) || !parse_resolved(resolved))
+    return nullptr;
+  const verify_fn_t verify = reinterpret_cast<verify_fn_t>(uintptr_t(vaddr));
+  PyObject* seq = PySequence_Fast(reqs, "auth_core_batch needs a sequence of requests");
+  if (!seq) return nullptr;
+  Batch b;
+  const double t0 = now_s();
+  if (collect_all(b, seq, clients, resolved, excluded) < 0) { Py_DECREF(seq); return nullptr; }
+  const double ta = now_s();
+  if (pack_all(b, threads) < 0) { Py_DECREF(seq); return nullptr; }
+  const double tb = now_s();
+  int rc = 0;
+  const size_t nf = b.items.size();
+  if (nf) {
+    uint8_t* base = b.ar->p;
+    Py_BEGIN_ALLOW_THREADS
+    // phase C: one device call
+    rc = verify(base, base + b.o_pk, base + b.o_msg, reinterpret_cast<const uint64_t*>(base + b.o_off), uint64_t(nf),
+                base + b.o_acc, mask);
+    Py_END_ALLOW_THREADS
+  }
+  Py_DECREF(seq);
+  if (rc != 0) {
+    PyErr_Format(PyExc_RuntimeError, "edv_verify_batch failed (%d)", rc);
+    return nullptr;
+  }
+  const double tc = now_s();
+  PyObject* res = build_output(b, false);
+  g_phase_s[0] = ta - t0;
+  g_phase_s[1] = tb - ta;
+  g_phase_s[2] = tc - tb;
+  g_phase_s[3] = now_s() - tc;
+  return res;
+}
+
+// ---- asynchronous whole batch (row f-2: the Node keeps going while the GPU works)
+// auth_core_submit(reqs, clients, excluded, submit_addr, wait_addr, device, threads, resolved, want_digests)
+//   -> handle: phases A and B as auth_core_batch, then ONE queued device call
+//   (edv_verify_digest_batch_async at submit_addr) that returns at once;
+// auth_core_finish(handle) -> (out, slow, rejected, digests or None): waits
+//   (edv_wait_async at wait_addr, GIL released) and builds the lists.  With
+//   want_digests, digests[k] is Request.getDigest() of request k when its signing
+//   bytes are its signingState serialization (digest_is_signing_bytes), computed
+//   on the device from the same bytes; None otherwise (the caller's digest path).
+// A handle dropped unfinished waits for its batch before its arena is reused.
+const char kBatchCapsule[] = "edv.auth_batch";
+
+void batch_capsule_free(PyObject* cap) {
+  Batch* b = static_cast<Batch*>(PyCapsule_GetPointer(cap, kBatchCapsule));
+  if (!b) { PyErr_Clear(); return; }
+  if (b->pending && b->wait) {
+    Py_BEGIN_ALLOW_THREADS
+    (void)b->wait(b->device, b->ticket);  // the device may still write into the arena
+    Py_END_ALLOW_THREADS
+  }
+  delete b;
+}
+
+PyObject* py_auth_core_submit(PyObject*, PyObject* args) {
+  PyObject *reqs, *clients, *excluded, *resolved = Py_None;
+  unsigned long long saddr, waddr;
+  int device, threads, want = 0;
+  if (!PyArg_ParseTuple(args, "OO!OKKii|Op", &reqs, &PyDict_Type, &clients, &excluded, &saddr, &waddr, &device,
+                        &threads, &resolved, &want) || !parse_resolved(resolved))
+    return nullptr;
+  PyObject* seq = PySequence_Fast(reqs, "auth_core_submit needs a sequence of requests");
+  if (!seq) return nullptr;
+  Batch* b = new Batch();
+  b->want_dig = want != 0;
+  b->device = device;
+  b->wait = reinterpret_cast<wait_fn_t>(uintptr_t(waddr));
+  PyObject* cap = PyCapsule_New(b, kBatchCapsule, batch_capsule_free);
+  if (!cap) { delete b; Py_DECREF(seq); return nullptr; }
+  if (collect_all(*b, seq, clients, resolved, excluded) < 0 || pack_all(*b, threads) < 0) {
+    Py_DECREF(seq);
+    Py_DECREF(cap);
+    return nullptr;
+  }
+  Py_DECREF(seq);
+  const size_t nf = b->items.size();
+  if (!nf) return cap;
+  const submit_fn_t submit = reinterpret_cast<submit_fn_t>(uintptr_t(saddr));
+  uint8_t* base = b->ar->p;
+  int64_t ticket = -1;
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = submit(base, base + b->o_pk, base + b->o_msg, reinterpret_cast<const uint64_t*>(base + b->o_off),
+              uint64_t(nf), base + b->o_acc, b->want_dig ? base + b->o_dig : nullptr, device, &ticket);
+  Py_END_ALLOW_THREADS
+  if (rc != 0) {
+    Py_DECREF(cap);
+    PyErr_Format(PyExc_RuntimeError, "edv_verify_digest_batch_async failed (%d)", rc);
+    return nullptr;
+  }
+  b->ticket = ticket;
+  b->pending = true;
+  return cap;
+}
+
+PyObject* py_auth_core_finish(PyObject*, PyObject* cap) {
+  Batch* b = static_cast<Batch*>(PyCapsule_GetPointer(cap, kBatchCapsule));
+  if (!b) return nullptr;
+  if (b->pending) {
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = b->wait(b->device, b->ticket);
+    Py_END_ALLOW_THREADS
+    b->pending = false;
+    if (rc != 0) {
+      PyErr_Format(PyExc_RuntimeError, "edv_wait_async failed (%d)", rc);
+      return nullptr;
+    }
+  }
+  return build_output(*b, b->want_dig);
 }
 
 // ------------------------------------------------- request digests (f-3)
@@ -834,7 +1010,6 @@ fail:
 // identifier -- the reference derives one from the signatures --, or a value
 // the native serializer leaves to Python); the caller computes those in Python.
 typedef int (*sha_fn_t)(const uint8_t*, const uint64_t*, uint64_t, uint8_t*, uint32_t);
-PyObject *g_k_reqid, *g_k_operation, *g_k_protocol;
 
 PyObject* py_request_digests(PyObject*, PyObject* args) {
   PyObject* reqs;
@@ -930,6 +1105,10 @@ PyMethodDef kMethods[] = {
     {"auth_core_batch", py_auth_core_batch, METH_VARARGS,
      "whole-batch CoreAuthNr fast path with the GPU verify inside: (out, slow, rejected)"},
     {"last_phases", py_last_phases, METH_NOARGS, "phase seconds of the last auth_core_batch call"},
+    {"auth_core_submit", py_auth_core_submit, METH_VARARGS,
+     "asynchronous auth_core_batch (+ Request digests): queue the device call, return a handle"},
+    {"auth_core_finish", py_auth_core_finish, METH_O,
+     "wait for an auth_core_submit handle: (out, slow, rejected, digests or None)"},
     {"set_host_allocator", py_set_host_allocator, METH_VARARGS,
      "page-locked arena allocator (edv_host_alloc, edv_host_free addresses)"},
     {"prep_core_batch", py_prep_core_batch, METH_VARARGS, "CoreAuthNr single-signature fast path (None = Python)"},
@@ -954,6 +1133,8 @@ PyMODINIT_FUNC PyInit__edvhost(void) {
   g_k_reqid = PyUnicode_InternFromString("reqId");
   g_k_operation = PyUnicode_InternFromString("operation");
   g_k_protocol = PyUnicode_InternFromString("protocolVersion");
+  g_k_signatures = PyUnicode_InternFromString("signatures");
+  g_k_fees = PyUnicode_InternFromString("fees");
   if (!g_k_identifier || !g_k_signature || !g_k_verkey) return nullptr;
   return PyModule_Create(&kModule);
 }

@@ -320,6 +320,10 @@ struct PinnedBuf {
 // fills every SIMD).  Sub-batch stream q uses scratch slots [q*P, (q+1)*P) of
 // the chunk state.
 constexpr int kQ = 4;
+// In-flight batches of the asynchronous host path per device: a Node keeps one
+// per prod in flight, and a pool of nodes in one process (C5) one per node, so
+// eight slots let up to eight callers overlap before a submission has to wait.
+constexpr int kAsyncSlots = 8;
 
 // One set of per-chunk state buffers (ChunkState storage + bucket permutation).
 struct ChunkBufs {
@@ -357,19 +361,21 @@ struct DevCtx {
   // split-prep host path (run_shard_split): copies on hcp, part q's prep on hs[q]
   hipStream_t hcp = nullptr;
   hipEvent_t part_copied[kQ] = {}, part_prepped[kQ] = {};
-  // asynchronous host path (edv_verify_batch_async): two slots used in turn,
+  // asynchronous host path (edv_verify_batch_async): kAsyncSlots slots used in turn,
   // H2D copies on hcp, kernels and the verdicts' D2H on hac, so the copies of
   // batch k+1 run while batch k computes
   struct AsyncSlot {
-    DevBuf sigs, pks, msgs, off, acc;
-    PinnedBuf stage, acc_host;
+    DevBuf sigs, pks, msgs, off, acc, dig;
+    PinnedBuf stage, acc_host, dig_host;
     hipEvent_t copied = nullptr, done = nullptr;
     int64_t ticket = -1;         // batch held by the slot, -1 = none
     uint8_t* accept = nullptr;   // the caller's verdict buffer
+    uint8_t* digests = nullptr;  // the caller's SHA-256 buffer (null: none asked for)
     uint64_t n = 0;
     bool acc_pinned = false;     // verdicts DMA'd straight into `accept`
+    bool dig_pinned = false;     // digests DMA'd straight into `digests`
   };
-  AsyncSlot as[2];
+  AsyncSlot as[kAsyncSlots];
   hipStream_t hac = nullptr;
   int64_t next_ticket = 0;
   DevBuf sigs, pks, msgs, off, acc;
@@ -898,6 +904,7 @@ int async_complete(DevCtx::AsyncSlot& s) {
   if (s.ticket < 0) return 0;
   HIPOK(hipEventSynchronize(s.done), "async wait");
   if (!s.acc_pinned) memcpy(s.accept, s.acc_host.p, s.n);
+  if (s.digests && !s.dig_pinned) memcpy(s.digests, s.dig_host.p, 32 * s.n);
   s.ticket = -1;
   return 0;
 }
@@ -905,18 +912,20 @@ int async_complete(DevCtx::AsyncSlot& s) {
 // Queue one host batch: H2D copies on hcp (from the caller's memory when it is
 // pinned, else through the slot's pinned staging, filled here while the
 // previous batch computes), then on hac the kernels and the D2H of the
-// verdicts.  A slot is reused two submissions later, after its batch is
+// verdicts.  A slot is reused kAsyncSlots submissions later, after its batch is
 // complete.  Caller holds c.mu.
 int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
-                 uint64_t n, uint8_t* accept, int64_t* ticket) {
+                 uint64_t n, uint8_t* accept, uint8_t* digests, int64_t* ticket) {
   const int64_t t = c.next_ticket;
-  DevCtx::AsyncSlot& s = c.as[t & 1];
+  DevCtx::AsyncSlot& s = c.as[t % kAsyncSlots];
   int err;
-  if ((err = async_complete(s))) return err;  // the batch of two submissions ago
+  if ((err = async_complete(s))) return err;  // the batch of kAsyncSlots submissions ago
   const uint64_t mbase = off[0], mbytes = off[n] - mbase;
   if (s.sigs.ensure(n * 64) || s.pks.ensure(n * 32) || s.msgs.ensure(mbytes + 64) || s.off.ensure((n + 1) * 8) ||
-      s.acc.ensure(n))
+      s.acc.ensure(n) || (digests && s.dig.ensure(32 * n)))
     return EDV_E_OOM;
+  s.dig_pinned = digests && is_pinned(digests);
+  if (digests && !s.dig_pinned && s.dig_host.ensure(32 * n)) return EDV_E_OOM;
   const bool pinned = is_pinned(sigs) && is_pinned(pks) && is_pinned(off) && (mbytes == 0 || is_pinned(msgs + mbase));
   s.acc_pinned = is_pinned(accept);
   if (!s.acc_pinned && s.acc_host.ensure(n)) return EDV_E_OOM;
@@ -947,9 +956,18 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
     return err;
   uint8_t* h_acc = s.acc_pinned ? accept : static_cast<uint8_t*>(s.acc_host.p);
   HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, c.hac), "d2h accept");
+  if (digests) {
+    // Request.getDigest of requests whose signing bytes ARE the message (the
+    // caller decides which): SHA-256 of the same resident message bytes
+    uint8_t* d_dig = static_cast<uint8_t*>(s.dig.p);
+    if ((err = launch_sha256(d_msgs, d_off, mbase, n, d_dig, c.hac))) return err;
+    uint8_t* h_dig = s.dig_pinned ? digests : static_cast<uint8_t*>(s.dig_host.p);
+    HIPOK(hipMemcpyAsync(h_dig, d_dig, 32 * n, hipMemcpyDeviceToHost, c.hac), "d2h digests");
+  }
   HIPOK(hipEventRecord(s.done, c.hac), "record");
   s.ticket = t;
   s.accept = accept;
+  s.digests = digests;
   s.n = n;
   c.next_ticket = t + 1;
   *ticket = t;
@@ -1077,6 +1095,12 @@ int edv_verify_batch(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msg
 
 int edv_verify_batch_async(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* msg_off,
                            uint64_t n, uint8_t* accept, int device, int64_t* ticket) {
+  return edv_verify_digest_batch_async(sigs, pks, msgs, msg_off, n, accept, nullptr, device, ticket);
+}
+
+int edv_verify_digest_batch_async(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                                  const uint64_t* msg_off, uint64_t n, uint8_t* accept, uint8_t* digests, int device,
+                                  int64_t* ticket) {
   g_err.clear();
   if (!ticket) return set_err(EDV_E_ARG, "null ticket");
   if (n > 0 && (!sigs || !pks || !msg_off || !accept)) return set_err(EDV_E_ARG, "null pointer");
@@ -1089,7 +1113,7 @@ int edv_verify_batch_async(const uint8_t* sigs, const uint8_t* pks, const uint8_
     *ticket = cl.c->next_ticket++;
     return 0;
   }
-  if ((err = submit_async(*cl.c, sigs, pks, msgs, msg_off, n, accept, ticket))) {
+  if ((err = submit_async(*cl.c, sigs, pks, msgs, msg_off, n, accept, digests, ticket))) {
     // whatever was queued before the failure may still read the caller's
     // buffers: let it finish before the caller gets the error back
     (void)hipStreamSynchronize(cl.c->hcp);

@@ -74,6 +74,9 @@ def lib():
         h.edv_verify_batch_dev_pipelined.restype = ctypes.c_int
         h.edv_verify_batch_async.argtypes = [vp, vp, vp, vp, u64, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
         h.edv_verify_batch_async.restype = ctypes.c_int
+        h.edv_verify_digest_batch_async.argtypes = [vp, vp, vp, vp, u64, vp, vp, ctypes.c_int,
+                                                    ctypes.POINTER(ctypes.c_int64)]
+        h.edv_verify_digest_batch_async.restype = ctypes.c_int
         h.edv_wait_async.argtypes = [ctypes.c_int, ctypes.c_int64]
         h.edv_wait_async.restype = ctypes.c_int
         h.edv_pipeline_sync.argtypes = [ctypes.c_int]
@@ -289,6 +292,24 @@ def verify_address() -> int:
                                     ctypes.cast(h.edv_host_free, ctypes.c_void_p).value)
         _verify_addr = ctypes.cast(h.edv_verify_batch, ctypes.c_void_p).value
     return _verify_addr
+
+
+_async_addrs = None
+
+
+def async_addresses():
+    """(edv_verify_digest_batch_async, edv_wait_async) addresses for the native
+    asynchronous whole-batch path (_edvhost.auth_core_submit / _finish)."""
+    global _async_addrs
+    if _async_addrs is None:
+        verify_address()  # page-locked arenas
+        h = lib()
+        _async_addrs = (ctypes.cast(h.edv_verify_digest_batch_async, ctypes.c_void_p).value,
+                        ctypes.cast(h.edv_wait_async, ctypes.c_void_p).value)
+    return _async_addrs
+
+
+BATCH_DEVICE = 0               # device of the native asynchronous whole-batch path
 
 
 def sha256_address() -> int:

@@ -88,6 +88,45 @@ def authenticate_prod(authenticator: ReqAuthenticator, client_msgs: Sequence[Tup
         on_client(msg, frm, _outcome(lambda: b.result(t)))
 
 
+class PendingProd:
+    """One prod's REQUESTs and PROPAGATEs submitted for authentication (and
+    their request digests) without waiting: finish() hands each message its
+    outcome in arrival order, as authenticate_prod does, one prod later."""
+
+    def __init__(self, authenticator: ReqAuthenticator, client_msgs, propagates, digests: bool = True):
+        self.client_msgs, self.propagates = list(client_msgs), list(propagates)
+        self.reqs = [m["request"] for m, _frm in self.propagates] + [m for m, _frm in self.client_msgs]
+        self._pending = authenticator.authenticate_batch_submit(self.reqs, digests=digests) if self.reqs else None
+
+    def digests(self, digest_fn=None):
+        """Request.getDigest of every request (propagates first): the device's,
+        and digest_fn's for the ones it did not hash."""
+        if self._pending is None:
+            return []
+        d = list(self._pending.digests())
+        rest = [k for k, x in enumerate(d) if x is None]
+        if rest:
+            if digest_fn is None:
+                raise ValueError("digests missing and no digest_fn")
+            for k, x in zip(rest, digest_fn([self.reqs[k] for k in rest])):
+                d[k] = x
+        return d
+
+    def finish(self, on_client, on_propagate):
+        res = self._pending.result() if self._pending is not None else []
+        it = iter(res)
+        for msg, frm in self.propagates:
+            on_propagate(msg, frm, _as_outcome(next(it)))
+        for msg, frm in self.client_msgs:
+            on_client(msg, frm, _as_outcome(next(it)))
+
+
+def _as_outcome(r):
+    """authenticate_batch's per-request result: the identifier set, or the
+    exception instance verifySignature would raise."""
+    return r
+
+
 def _outcome(f):
     try:
         return f()
@@ -99,4 +138,4 @@ def failed(outcome) -> Optional[BaseException]:
     return outcome if isinstance(outcome, BaseException) else None
 
 
-__all__: List[str] = ["DEFAULT_LISTENER_QUOTA", "ProdAuthBatch", "authenticate_prod", "failed"]
+__all__: List[str] = ["DEFAULT_LISTENER_QUOTA", "PendingProd", "ProdAuthBatch", "authenticate_prod", "failed"]

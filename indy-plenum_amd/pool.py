@@ -26,20 +26,19 @@ prod's client REQUESTs and PROPAGATEs through ONE authenticate_batch call
 one-message-at-a-time verifySignature.  Request keys are Request.getDigest
 (request.py:71-72) values computed by `digest_fn`.
 
-`overlap=True` (batched only) submits a prod's digest + authentication batch to
-a background thread and handles its verdicts at the node's next prod, so the
-GPU round trip of one node's batch runs while the nodes do their Python work
-(the native batch call releases the GIL for base58 decoding and the device
-call).  Each message is still handled exactly once with its own verdict, in
-arrival order; it is only handled one prod later.
+`overlap=True` (batched only) submits a prod's authentication batch without
+waiting (ReqAuthenticator.authenticate_batch_submit: host prep now, one queued
+device call that also hashes the request digests) and handles its verdicts at
+the node's next prod, so the GPU round trip of one node's batch runs while the
+nodes do their Python work.  Each message is still handled exactly once with
+its own verdict, in arrival order; it is only handled one prod later.
 """
 import hashlib
 import json
 import time
 from collections import deque
-from concurrent.futures import ThreadPoolExecutor
 
-from .node_integration import DEFAULT_LISTENER_QUOTA, authenticate_prod, failed
+from .node_integration import DEFAULT_LISTENER_QUOTA, PendingProd, authenticate_prod, failed
 from .signing_serializer import serialize_msg_for_signing
 from .digest import signing_state
 
@@ -86,14 +85,18 @@ class _TimedAuth:
         finally:
             self._node.auth_s += time.perf_counter() - t
 
+    def authenticate_batch_submit(self, reqs, digests=False):
+        # timed by the caller (PoolNode.prod), together with the hand-over
+        return self._auth.authenticate_batch_submit(reqs, digests=digests)
+
 
 class PoolNode:
     def __init__(self, name, peers, authenticator, f, batched=True, digest_fn=cpu_digests,
                  client_quota=DEFAULT_LISTENER_QUOTA, node_quota=DEFAULT_LISTENER_QUOTA, max_batch=1000,
-                 executor=None):
+                 overlap=False):
         self.name, self.peers, self.f = name, list(peers), f
-        self.executor = executor if batched else None  # overlap mode: the pool's background thread
-        self._pending = None          # (future, clients, props) of the previous prod (overlap mode)
+        self.overlap = overlap and batched
+        self._pending = None          # PendingProd of the previous prod (overlap mode)
         self.auth = _TimedAuth(authenticator, self)
         self.n = len(self.peers) + 1
         self.batched, self.digest_fn = batched, digest_fn
@@ -144,17 +147,16 @@ class PoolNode:
                 (props if m["op"] == "PROPAGATE" else three_pc).append((m, frm))
         clients = [(json.loads(self.client_inbox.popleft()), "client")
                    for _ in range(min(self.client_quota, len(self.client_inbox)))]
-        if self.executor is not None:
+        if self.overlap:
             pend, self._pending = self._pending, None
             if props or clients:
                 self.verifies += len(props) + len(clients)
                 self.auth_calls += 1
-                reqs = [m["request"] for m, _ in props] + [m for m, _ in clients]
                 ta = time.perf_counter()
-                self._pending = (self.executor.submit(self._digest_and_auth, reqs), clients, props)
+                self._pending = PendingProd(self.auth, clients, props, digests=True)
                 self.auth_s += time.perf_counter() - ta
             if pend is not None:
-                self._finish(*pend)
+                self._finish(pend)
         elif props or clients:
             ta = time.perf_counter()
             keys = self.digest_fn([m["request"] for m, _ in props] + [m for m, _ in clients])
@@ -171,21 +173,14 @@ class PoolNode:
         self.busy_s += time.perf_counter() - t0
         return n_work
 
-    # overlap mode: one prod's digests and verdicts, computed in the background
-    def _digest_and_auth(self, reqs):
-        keys = self.digest_fn(reqs)
-        return keys, self.auth._auth.authenticate_batch(reqs)
-
-    def _finish(self, fut, clients, props):
+    # overlap mode: the previous prod's verdicts and digests, handed over now
+    def _finish(self, pend):
         ta = time.perf_counter()
-        keys, results = fut.result()      # the node thread waits only for what did not overlap
+        # waits only for what did not overlap, and builds the verdict lists
+        keys = pend.digests(self.digest_fn)
         self.auth_s += time.perf_counter() - ta
         self._keys = iter(keys)
-        it = iter(results)
-        for msg, frm in props:
-            self._on_propagate(msg, frm, _as_outcome(next(it)))
-        for msg, frm in clients:
-            self._on_client(msg, frm, _as_outcome(next(it)))
+        pend.finish(self._on_client, self._on_propagate)
 
     # ------------------------------------------------------- requests
     def _on_client(self, req, frm, outcome):
@@ -297,10 +292,8 @@ class Pool:
     def __init__(self, auth_factory, n=4, batched=True, digest_fn=cpu_digests, overlap=False, **node_kw):
         names = NAMES[:n]
         f = (n - 1) // 3
-        # one background thread: batches of different nodes reach the device one at a time
-        self.executor = ThreadPoolExecutor(max_workers=1) if overlap and batched else None
         self.nodes = {nm: PoolNode(nm, [p for p in names if p != nm], auth_factory(nm), f, batched, digest_fn,
-                                   executor=self.executor, **node_kw) for nm in names}
+                                   overlap=overlap, **node_kw) for nm in names}
         self.nodes[names[0]].is_primary = True
 
     def submit(self, reqs):
@@ -334,11 +327,8 @@ class Pool:
                 nd._finish(*pend)
 
     def close(self):
-        """Stop the overlap mode's background thread (the pool is unusable after)."""
+        """Hand over whatever is still in flight (the pool stays usable)."""
         self.drain()
-        if self.executor is not None:
-            self.executor.shutdown(wait=True)
-            self.executor = None
 
     def stats(self, wall_s, n_reqs):
         nodes = list(self.nodes.values())

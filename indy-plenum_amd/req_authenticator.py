@@ -76,12 +76,12 @@ class ReqAuthenticator:
         with gc_paused():
             return self._authenticate_batch(reqs)
 
-    def _single_stock(self, reqs):
+    def _single_stock_plan(self, reqs):
         """Fast path for the usual node set-up, one authenticator whose batch path
         is the stock read-only one: list-comprehension passes only, the type
-        predicates evaluated once per distinct type.  None = use the general path
-        (several authenticators, a malformed request, an unhashable type, a
-        predicate that raises)."""
+        predicates evaluated once per distinct type.  -> (authenticator, todo,
+        kinds) or None = use the general path (several authenticators, a
+        malformed request, an unhashable type, a predicate that raises)."""
         if len(self._authenticators) != 1:
             return None
         a = self._authenticators[0]
@@ -94,9 +94,11 @@ class ReqAuthenticator:
         except Exception:
             return None
         kd = [kinds[t] for t in typs]
-        todo = [k for k, x in enumerate(kd) if x == 2]
+        return a, [k for k, x in enumerate(kd) if x == 2], kd
+
+    @staticmethod
+    def _single_stock_out(kd, todo, results):
         out = [set() if x == 0 else None for x in kd]
-        results = a.authenticate_batch([reqs[k] for k in todo])
         for k, rv in zip(todo, results):
             # authenticate(): identifiers.update(rv or set()); none -> NoAuthenticatorFound
             out[k] = rv if isinstance(rv, BaseException) else (set(rv) if rv else NoAuthenticatorFound())
@@ -104,6 +106,39 @@ class ReqAuthenticator:
             if x == 1:
                 out[k] = NoAuthenticatorFound()
         return out
+
+    def _single_stock(self, reqs):
+        plan = self._single_stock_plan(reqs)
+        if plan is None:
+            return None
+        a, todo, kd = plan
+        return self._single_stock_out(kd, todo, a.authenticate_batch([reqs[k] for k in todo]))
+
+    def authenticate_batch_submit(self, reqs, digests: bool = False):
+        """Asynchronous authenticate_batch (the Node's prod keeps going while the
+        GPU verifies): -> PendingAuth whose result() is authenticate_batch(reqs)
+        and whose digests() holds Request.getDigest for the requests the device
+        hashed (None elsewhere).  Only the single stock authenticator submits
+        asynchronously; any other set-up is authenticated at once."""
+        from .client_authn import PendingAuth
+        plan = self._single_stock_plan(reqs)
+        if plan is None or not hasattr(plan[0], "authenticate_batch_submit"):
+            out = self.authenticate_batch(reqs)
+            return PendingAuth(lambda: (out, [None] * len(reqs)))
+        a, todo, kd = plan
+        sub = [reqs[k] for k in todo]
+        with gc_paused():
+            p = a.authenticate_batch_submit(sub, digests=digests)
+
+        def finish():
+            with gc_paused():
+                res = p.result()
+                out = self._single_stock_out(kd, todo, res)
+            dig = [None] * len(reqs)
+            for k, d in zip(todo, p.digests()):
+                dig[k] = d
+            return out, dig
+        return PendingAuth(finish)
 
     def _authenticate_batch(self, reqs):
         fast = self._single_stock(reqs)

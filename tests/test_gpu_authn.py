@@ -62,3 +62,42 @@ def test_gpu_whole_batch_native_path(monkeypatch):
     got = auth.authenticate_batch(reqs)
     got = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in got]
     assert got == want
+
+
+def test_gpu_async_submit_with_digests_and_state(monkeypatch):
+    """authenticate_batch_submit on the real GPU (native prep, ONE queued
+    edv_verify_digest_batch_async call, wait at result()): the sequential
+    reference chain's outcomes, Request.getDigest for every request the device
+    hashed, and state-backed verkeys (client_authn.py:148-160) on the same
+    native path.  Several batches in flight at once (as the pool's nodes keep
+    them), finished out of order."""
+    import json
+    from indy_plenum_amd.client_authn import nym_to_state_key
+    from indy_plenum_amd.pool import cpu_digests
+    auth, reqs = H.make_requests(2400, seed=43)
+
+    class St:
+        kv = {}
+
+        def get(self, key, isCommitted=True):
+            assert isCommitted is False
+            return self.kv.get(key)
+    st = St()
+    for idr in list(auth.clients)[:5]:
+        st.kv[nym_to_state_key(idr)] = json.dumps(auth.clients.pop(idr)).encode()
+    auth.state = st
+    want = _sequential_on_oracle(lambda: [H.outcome(lambda r=r: auth.authenticate(r)) for r in reqs], monkeypatch)
+    assert edv.native_batch_enabled()
+    norm = lambda res: [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x)
+                        for x in res]
+    parts = [reqs[k::4] for k in range(4)]
+    pend = [auth.authenticate_batch_submit(p, digests=True) for p in parts]
+    for k in (2, 0, 3, 1):
+        got = norm(pend[k].result())
+        assert got == want[k::4]
+        hashed = 0
+        for q, d in zip(parts[k], pend[k].digests()):
+            if d is not None:
+                hashed += 1
+                assert d == cpu_digests([q])[0]
+        assert hashed > 300

@@ -4,7 +4,7 @@
 * scratch ordering across caller streams (two batches in flight on two
   streams at once must each get their own verdicts);
 * the host path: pinned (edv_host_alloc) and pageable inputs, sub-batches,
-  chunk seams, the opt-in split-prep mode and the asynchronous two-slot path;
+  chunk seams, the opt-in split-prep mode and the asynchronous slotted path;
 * the multi-device path (one host thread per device, edv_shard_split) on
   EDV_VIRTUAL_DEVICES logical devices, against libsodium's committed bitmask
   (C3 split by request index) and the checker (C4 cost-balanced split);
@@ -181,24 +181,26 @@ def _pinned_copy(sigs, pks, msgs, off, n):
 def test_host_async_path():
     """edv_verify_batch_async / edv_wait_async: batches of fixed and mixed
     lengths (sizes 20,000 / 4,097 / 65,536 / 1 / 30,000, 15 % invalid) queued
-    back to back from pageable memory, waits one behind, a slot reused without
-    an explicit wait (the submission completes the batch two back), then pinned
-    inputs with pinned verdict buffers in turn; every batch equals the checker."""
+    back to back from pageable memory, twice over (ten in flight: slots reused
+    without an explicit wait, the submission completing the batch eight back),
+    then pinned inputs with pinned verdict buffers in turn; every batch equals
+    the checker."""
     sizes = (20000, 4097, 65536, 1, 30000)
     batches = [orc.corpus(0xA5A0 + k, 0, n, mode=k % 2, invalid_permille=150) for k, n in enumerate(sizes)]
     wants = [checker(*b) for b in batches]
-    accs = [np.full(n, 7, np.uint8) for n in sizes]
+    order = list(range(5)) * 2
+    accs = [np.full(sizes[k], 7, np.uint8) for k in order]
     tickets = []
-    for k, b in enumerate(batches):
-        tickets.append(edv.verify_async(*b, accs[k]))
-        if k == 1:
+    for j, k in enumerate(order):
+        tickets.append(edv.verify_async(*batches[k], accs[j]))
+        if j == 1:
             edv.wait_async(tickets[0])
             assert np.array_equal(accs[0], wants[0])
-    # tickets 1 and 2 were completed by the submissions two after them; waiting is still fine
+    # tickets 1 and 2 were completed by the submissions eight after them; waiting is still fine
     for t in tickets:
         edv.wait_async(t)
-    for a, w in zip(accs, wants):
-        assert np.array_equal(a, w)
+    for j, k in enumerate(order):
+        assert np.array_equal(accs[j], wants[k])
     with pytest.raises(edv.EdvError):
         edv.wait_async(tickets[-1] + 100)
     # pinned inputs and verdicts: DMA straight from and into the caller's memory

@@ -394,3 +394,129 @@ def test_whole_batch_native_path_with_state_verkeys(monkeypatch, n_keys_on_devic
     assert sum(slow_calls) == 0                       # the odd ones fail before any verify
     assert {o[1] for o in got if o[0] == "raise"} >= {"UnknownIdentifier", "CouldNotAuthenticate",
                                                       "InsufficientCorrectSignatures"}
+
+
+def _oracle_async_callbacks(calls):
+    """edv_verify_digest_batch_async / edv_wait_async-compatible C function
+    pointers backed by the oracle and hashlib: the batch is 'done' at submit,
+    wait checks the ticket.  Lets the asynchronous native path run on the CPU."""
+    import ctypes
+    import hashlib
+    import oracle_lib as orc
+    SUB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                           ctypes.POINTER(ctypes.c_int64))
+    WAIT = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.c_int64)
+    issued = []
+
+    def submit(sigs, pks, msgs, off, n, acc, digests, device, ticket):
+        o = np.ctypeslib.as_array((ctypes.c_uint64 * (n + 1)).from_address(off)).copy()
+        blob = ctypes.string_at(msgs, int(o[-1]) + 16)
+        res = orc.verify_batch(ctypes.string_at(sigs, 64 * n), ctypes.string_at(pks, 32 * n), blob, o, n, 4)
+        ctypes.memmove(acc, res, n)
+        if digests:
+            d = b"".join(hashlib.sha256(blob[int(o[i]) - int(o[0]):int(o[i + 1]) - int(o[0])]).digest()
+                         for i in range(n))
+            ctypes.memmove(digests, d, 32 * n)
+        calls.append((n, bool(digests)))
+        ticket[0] = len(issued)
+        issued.append(False)
+        return 0
+
+    def wait(device, ticket):
+        if not 0 <= ticket < len(issued) or issued[ticket]:
+            return -1
+        issued[ticket] = True
+        return 0
+    cbs = (SUB(submit), WAIT(wait))
+    return cbs, tuple(ctypes.cast(c, ctypes.c_void_p).value for c in cbs), issued
+
+
+@pytest.mark.parametrize("with_state", [False, True])
+def test_async_submit_finish_equals_sequential_with_digests(monkeypatch, with_state):
+    """authenticate_batch_submit -> PendingAuth (native phases A/B, one queued
+    device call with the request digests, finish = wait + output): the same
+    per-request results as the sequential reference chain, and digests equal to
+    Request.getDigest (hashlib over the reference restatement) exactly for the
+    requests whose signing bytes are their signingState serialization, None for
+    the rest.  Also through ReqAuthenticator and node_integration.PendingProd."""
+    import json
+    import test_authn_host as H
+    from indy_plenum_amd import client_authn, digest
+    from indy_plenum_amd.client_authn import nym_to_state_key
+    from indy_plenum_amd.node_integration import PendingProd
+    from indy_plenum_amd.pool import cpu_digests
+    from indy_plenum_amd.req_authenticator import ReqAuthenticator
+    sa, reqs = H.make_requests(1500, seed=57)
+    r = random.Random(5)
+    for q in reqs[::7]:
+        q["extra"] = 1                               # signing bytes != signingState: no device digest
+    for q in reqs[3::11]:
+        if isinstance(q, dict):
+            q["protocolVersion"] = None              # signingState drops it, the signing bytes keep it
+    if with_state:
+        st = _RecordingState()
+        for idr in list(sa.clients)[:4]:             # some identifiers only in the state
+            st.kv[nym_to_state_key(idr)] = json.dumps(sa.clients.pop(idr)).encode()
+        sa.state = st
+    with monkeypatch.context() as m:
+        m.setattr(edv, "open_batch", H.oracle_open_batch)
+        want = [H.outcome(lambda q=q: sa.authenticate(q)) for q in reqs]
+    calls = []
+    cbs, addrs, issued = _oracle_async_callbacks(calls)
+    monkeypatch.setattr(edv, "async_addresses", lambda: addrs)
+    monkeypatch.setattr(edv, "verify_address", lambda: addrs[0])
+    monkeypatch.setattr(client_authn.CoreAuthMixin, "STATE_KEYS_ON_DEVICE", 10**9)
+
+    def counting_open(items, device_mask=0):
+        return H.oracle_open_batch(list(items))
+    monkeypatch.setattr(edv, "_OPEN_BATCH", counting_open)
+    monkeypatch.setattr(edv, "open_batch", counting_open)
+    norm = lambda res: [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x)
+                        for x in res]
+    p = sa.authenticate_batch_submit(reqs, digests=True)
+    assert len(calls) == 1 and calls[0][1] and issued == [False]   # queued, not waited for
+    assert norm(p.result()) == want and issued == [True]
+    digs = p.digests()
+    ref = cpu_digests([q for q in reqs if isinstance(q, dict) and q.get("identifier")])
+    got_some = 0
+    it = iter(ref)
+    for q, d in zip(reqs, digs):
+        if not (isinstance(q, dict) and q.get("identifier")):
+            assert d is None
+            continue
+        x = next(it)
+        if d is not None:
+            got_some += 1
+            assert d == x
+            assert "extra" not in q and q.get("protocolVersion", 0) is not None
+    assert got_some > 500
+    # through ReqAuthenticator (single stock authenticator) and PendingProd
+    ra = ReqAuthenticator()
+    ra.register_authenticator(sa)
+    with monkeypatch.context() as m:
+        m.setattr(edv, "open_batch", H.oracle_open_batch)
+        want_ra = [H.outcome(lambda q=q: ra.authenticate(q)) for q in reqs]
+    pr = ra.authenticate_batch_submit(reqs, digests=True)
+    assert norm(pr.result()) == want_ra
+    # requests ReqAuthenticator hands to the authenticator get the same digests; the
+    # others (queries, unknown types: never submitted) get None
+    assert all(d is None or d == e for d, e in zip(pr.digests(), digs))
+    assert sum(d is not None for d in pr.digests()) > 400
+    good = [q for q in reqs if isinstance(q, dict) and q.get("identifier")]
+    props = [({"op": "PROPAGATE", "request": q}, "Beta") for q in good[:300]]
+    clients = [(q, "client") for q in good[300:]]
+    seen = []
+    pp = PendingProd(ra, clients, props, digests=True)
+    assert pp.digests(cpu_digests) == cpu_digests(good)      # device digests + the digest_fn rest
+    pp.finish(lambda m, f, o: seen.append(("c", o)), lambda m, f, o: seen.append(("p", o)))
+    with monkeypatch.context() as m:
+        m.setattr(edv, "open_batch", H.oracle_open_batch)
+        want_pp = [H.outcome(lambda q=q: ra.authenticate(q)) for q in good]
+    assert norm([x for _k, x in seen]) == want_pp
+    # a handle dropped unfinished is waited for (no stray batch left in flight)
+    n_before = len(issued)
+    sa.authenticate_batch_submit(reqs[:50], digests=False)
+    import gc as _gc
+    _gc.collect()
+    assert len(issued) == n_before + 1 and issued[-1] is True

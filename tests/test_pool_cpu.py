@@ -92,3 +92,31 @@ def test_pool_stall_raises(batched, overlap, monkeypatch):
         assert [nd.ordered for nd in pool.nodes.values()] == [len(valid)] * 4
     finally:
         pool.close()
+
+
+def test_pool_overlap_on_the_native_async_path(monkeypatch):
+    """overlap=True through the real native asynchronous path (auth_core_submit /
+    auth_core_finish, device digests) with the device calls answered by the
+    oracle and hashlib: the same ordered set and NACKs as the reference flow."""
+    from test_host_native import _oracle_async_callbacks
+    calls = []
+    cbs, addrs, issued = _oracle_async_callbacks(calls)
+    monkeypatch.setattr(edv, "async_addresses", lambda: addrs)
+    monkeypatch.setattr(edv, "verify_address", lambda: addrs[0])
+    monkeypatch.setattr(edv, "_OPEN_BATCH", H.oracle_open_batch)
+    monkeypatch.setattr(edv, "open_batch", H.oracle_open_batch)
+    signers, reqs, valid = flood()
+    pool = Pool(factory(signers), n=4, batched=True, digest_fn=cpu_digests, overlap=True, client_quota=16,
+                max_batch=7)
+    pool.submit(reqs)
+    try:
+        wall = pool.run(len(valid))
+    finally:
+        pool.close()
+    st = pool.stats(wall, len(valid))
+    assert st["ordered_per_node"] == [len(valid)] * 4
+    assert st["nacks_per_node"] == [len(reqs) - len(valid)] * 4
+    keys = [nd.ordered_keys for nd in pool.nodes.values()]
+    assert all(k == keys[0] for k in keys) and keys[0] == set(cpu_digests(valid))
+    assert calls and all(d for _n, d in calls)          # every batch asked for device digests
+    assert all(issued)                                  # every queued batch was waited for

@@ -50,6 +50,18 @@ def make_flood(n, seed=0xC5):
     return clients, reqs
 
 
+class FreeAuthNr(CoreAuthNr):
+    """The ceiling: every request authenticated to its identifier with no
+    signature check at all (what the pool orders if verification cost
+    nothing).  Harness only; never a product path."""
+
+    def authenticate(self, req_data, identifier=None, signature=None, verifier=None):
+        return [req_data["identifier"]]
+
+    def authenticate_batch(self, reqs, verifier=None):
+        return [[r["identifier"]] for r in reqs]
+
+
 def factory(clients, cls):
     def make(_name):
         a = cls()
@@ -65,6 +77,8 @@ def run(mode, clients, reqs):
     if mode in ("gpu_batched", "gpu_batched_overlap"):
         pool = Pool(factory(clients, CoreAuthNr), n=4, batched=True, digest_fn=digest.request_digests,
                     overlap=mode == "gpu_batched_overlap")
+    elif mode == "no_verify_ceiling":
+        pool = Pool(factory(clients, FreeAuthNr), n=4, batched=True, digest_fn=digest.request_digests)
     else:
         pool = Pool(factory(clients, sodium_ref.SodiumCoreAuthNr), n=4, batched=False, digest_fn=cpu_digests)
     native = base58._native
@@ -88,7 +102,11 @@ def c5(n=20000, n_cpu=2000):
     run("gpu_batched", clients, reqs[:500])   # warm-up: tables, arenas, pinned staging
     out = {"metric": "4-node pool ordered requests/s under a client flood (C5)", "n_nodes": 4, "f": 1,
            "gpu_batched": run("gpu_batched", clients, reqs),
-           "gpu_batched_overlap": run("gpu_batched_overlap", clients, reqs)}
+           "gpu_batched_overlap": run("gpu_batched_overlap", clients, reqs),
+           "no_verify_ceiling": run("no_verify_ceiling", clients, reqs)}
+    ceil = out["no_verify_ceiling"]["ordered_req_per_s_one_process"]
+    out["overlap_vs_ceiling"] = out["gpu_batched_overlap"]["ordered_req_per_s_one_process"] / ceil
+    out["batched_vs_ceiling"] = out["gpu_batched"]["ordered_req_per_s_one_process"] / ceil
     if sodium_ref.sodium() is not None:
         out["cpu_reference"] = run("cpu_reference", clients, reqs[:n_cpu])
         g, c = out["gpu_batched"], out["cpu_reference"]
