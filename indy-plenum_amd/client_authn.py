@@ -428,6 +428,15 @@ class CoreAuthMixin:
         state = self.state
         if state is None:
             return None
+        if _edvhost is not None and hasattr(state, "get"):
+            # the same reads natively (state keys by a CPU SHA-256, the usual flat
+            # JSON value parsed in C, anything else through json.loads)
+            return _edvhost.state_nyms(reqs, self.clients, state.get, json.loads) or None
+        return self._state_nyms_py(reqs)
+
+    def _state_nyms_py(self, reqs):
+        """Python restatement of _edvhost.state_nyms (tests pin one against the other)."""
+        state = self.state
         clients = self.clients
         idrs = []
         seen = set()

@@ -998,6 +998,220 @@ PyObject* py_auth_core_finish(PyObject*, PyObject* cap) {
   return build_output(*b, b->want_dig);
 }
 
+// ------------------------------------- state-backed verkeys (P5, rows f-1/f-3)
+// state_nyms(reqs, clients, state_get, json_loads) -> {identifier: nym dict}
+// SimpleAuthNr.getVerkey's second source (client_authn.py:148-160 ->
+// domain_req_handler.py:158-167): for every distinct str identifier whose
+// `clients` entry is missing or falsy, state_get(sha256(identifier), False)
+// (nym_to_state_key; SHA-256 on the CPU here: one block per identifier), then
+// the JSON value.  The usual value -- one flat object of plain strings, numbers,
+// true/false/null -- is read here; anything else (escapes, nesting, non-ASCII,
+// malformed text, a non-bytes value) goes to json_loads exactly as the Python
+// restatement calls it.  Only non-empty objects are kept; for the fast-read ones
+// the dict holds the one field the batch path reads ("verkey": str) and is left
+// out when that is absent or not a string, so the Python plan raises what the
+// reference raises for them.
+#include "edv_sha256.h"
+
+// Strict JSON subset scanner: 1 = parsed (vk/vk_n set if a string "verkey" was
+// the last such key, *nkeys = member count), 0 = outside the subset.
+int scan_flat_json(const uint8_t* p, size_t n, const uint8_t** vk, size_t* vk_n, bool* vk_str, int* nkeys) {
+  size_t i = 0;
+  auto ws = [&]() { while (i < n && (p[i] == ' ' || p[i] == '\t' || p[i] == '\n' || p[i] == '\r')) i++; };
+  auto str = [&](const uint8_t** s, size_t* sn) -> bool {
+    if (i >= n || p[i] != '"') return false;
+    const size_t a = ++i;
+    while (i < n && p[i] != '"') {
+      if (p[i] < 0x20 || p[i] > 0x7e || p[i] == '\\') return false;
+      i++;
+    }
+    if (i >= n) return false;
+    *s = p + a;
+    *sn = i - a;
+    i++;
+    return true;
+  };
+  auto digits = [&]() -> bool {
+    const size_t a = i;
+    while (i < n && p[i] >= '0' && p[i] <= '9') i++;
+    return i > a;
+  };
+  auto number = [&]() -> bool {  // -?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?
+    if (i < n && p[i] == '-') i++;
+    if (i >= n) return false;
+    if (p[i] == '0') i++;
+    else if (p[i] >= '1' && p[i] <= '9') digits();
+    else return false;
+    if (i < n && p[i] == '.') { i++; if (!digits()) return false; }
+    if (i < n && (p[i] == 'e' || p[i] == 'E')) {
+      i++;
+      if (i < n && (p[i] == '+' || p[i] == '-')) i++;
+      if (!digits()) return false;
+    }
+    return true;
+  };
+  auto lit = [&](const char* w) -> bool {
+    const size_t k = strlen(w);
+    if (i + k > n || memcmp(p + i, w, k) != 0) return false;
+    i += k;
+    return true;
+  };
+  *vk = nullptr;
+  *vk_n = 0;
+  *vk_str = false;
+  *nkeys = 0;
+  ws();
+  if (i >= n || p[i] != '{') return 0;
+  i++;
+  ws();
+  if (i < n && p[i] == '}') {
+    i++;
+  } else {
+    for (;;) {
+      const uint8_t* k;
+      size_t kn;
+      ws();
+      if (!str(&k, &kn)) return 0;
+      ws();
+      if (i >= n || p[i] != ':') return 0;
+      i++;
+      ws();
+      if (i >= n) return 0;
+      const bool is_vk = kn == 6 && memcmp(k, "verkey", 6) == 0;
+      if (p[i] == '"') {
+        const uint8_t* v;
+        size_t vn;
+        if (!str(&v, &vn)) return 0;
+        if (is_vk) { *vk = v; *vk_n = vn; *vk_str = true; }
+      } else {
+        const bool ok = (p[i] == 'n' && lit("null")) || (p[i] == 't' && lit("true")) ||
+                        (p[i] == 'f' && lit("false")) || ((p[i] == '-' || (p[i] >= '0' && p[i] <= '9')) && number());
+        if (!ok) return 0;
+        if (is_vk) { *vk = nullptr; *vk_n = 0; *vk_str = false; }
+      }
+      (*nkeys)++;
+      ws();
+      if (i < n && p[i] == ',') { i++; continue; }
+      if (i < n && p[i] == '}') { i++; break; }
+      return 0;
+    }
+  }
+  ws();
+  return i == n ? 1 : 0;
+}
+
+PyObject* py_state_nyms(PyObject*, PyObject* args) {
+  PyObject *reqs, *clients, *state_get, *json_loads;
+  if (!PyArg_ParseTuple(args, "OO!OO", &reqs, &PyDict_Type, &clients, &state_get, &json_loads)) return nullptr;
+  PyObject* seq = PySequence_Fast(reqs, "state_nyms needs a sequence of requests");
+  if (!seq) return nullptr;
+  PyObject* out = PyDict_New();
+  PyObject* seen = PySet_New(nullptr);
+  if (!out || !seen) { Py_XDECREF(out); Py_XDECREF(seen); Py_DECREF(seq); return nullptr; }
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  std::vector<uint8_t> buf;
+  for (Py_ssize_t k = 0; k < n; k++) {
+    PyObject* req = PySequence_Fast_GET_ITEM(seq, k);
+    if (!PyDict_CheckExact(req)) continue;
+    PyObject* idr = PyDict_GetItem(req, g_k_identifier);
+    if (!idr || !PyUnicode_CheckExact(idr) || PyUnicode_GET_LENGTH(idr) == 0) continue;
+    const int s_in = PySet_Contains(seen, idr);
+    if (s_in < 0) goto fail;
+    if (s_in) continue;
+    if (PySet_Add(seen, idr) < 0) goto fail;
+    {
+      PyObject* c = PyDict_GetItemWithError(clients, idr);
+      if (!c && PyErr_Occurred()) goto fail;
+      if (c) {
+        const int t = PyObject_IsTrue(c);
+        if (t < 0) goto fail;
+        if (t) continue;  // getVerkey answers from the in-memory map
+      }
+    }
+    Py_ssize_t ulen;
+    const char* u = PyUnicode_AsUTF8AndSize(idr, &ulen);
+    if (!u) goto fail;
+    // nym_to_state_key: sha256(identifier.encode()), the kernel's SHA-256 on the CPU
+    buf.assign(size_t(ulen) + 48, 0);
+    memcpy(buf.data() + 16, u, size_t(ulen));
+    uint32_t d[8];
+    edv::sha256_msg(d, buf.data() + 16, uint64_t(ulen));
+    uint8_t key[32];
+    for (int w = 0; w < 8; w++) {
+      key[4 * w] = uint8_t(d[w]);
+      key[4 * w + 1] = uint8_t(d[w] >> 8);
+      key[4 * w + 2] = uint8_t(d[w] >> 16);
+      key[4 * w + 3] = uint8_t(d[w] >> 24);
+    }
+    PyObject* kb = PyBytes_FromStringAndSize(reinterpret_cast<const char*>(key), 32);
+    if (!kb) goto fail;
+    PyObject* data = PyObject_CallFunctionObjArgs(state_get, kb, Py_False, nullptr);
+    Py_DECREF(kb);
+    if (!data) goto fail;
+    const int truth = PyObject_IsTrue(data);
+    if (truth <= 0) {
+      Py_DECREF(data);
+      if (truth < 0) goto fail;
+      continue;
+    }
+    const uint8_t* txt = nullptr;
+    Py_ssize_t tn = 0;
+    if (PyBytes_CheckExact(data)) {
+      txt = reinterpret_cast<const uint8_t*>(PyBytes_AS_STRING(data));
+      tn = PyBytes_GET_SIZE(data);
+    } else if (PyUnicode_CheckExact(data) && PyUnicode_IS_ASCII(data)) {
+      txt = reinterpret_cast<const uint8_t*>(PyUnicode_DATA(data));
+      tn = PyUnicode_GET_LENGTH(data);
+    }
+    const uint8_t* vk;
+    size_t vk_n;
+    bool vk_str;
+    int nkeys;
+    PyObject* nym = nullptr;
+    if (txt && scan_flat_json(txt, size_t(tn), &vk, &vk_n, &vk_str, &nkeys)) {
+      if (nkeys > 0 && vk_str) {
+        nym = PyDict_New();
+        PyObject* v = nym ? PyUnicode_FromStringAndSize(reinterpret_cast<const char*>(vk), Py_ssize_t(vk_n)) : nullptr;
+        if (!v || PyDict_SetItem(nym, g_k_verkey, v) < 0) { Py_XDECREF(v); Py_XDECREF(nym); Py_DECREF(data); goto fail; }
+        Py_DECREF(v);
+      }
+    } else {
+      // the Python restatement's exact call: json.loads(bytes(data).decode() or data)
+      PyObject* arg = nullptr;
+      if (PyBytes_Check(data) || PyByteArray_Check(data)) {
+        arg = PyBytes_Check(data) ? PyUnicode_FromEncodedObject(data, "utf-8", "strict")
+                                  : PyUnicode_DecodeUTF8(PyByteArray_AS_STRING(data), PyByteArray_GET_SIZE(data), "strict");
+      } else {
+        Py_INCREF(data);
+        arg = data;
+      }
+      PyObject* v = arg ? PyObject_CallFunctionObjArgs(json_loads, arg, nullptr) : nullptr;
+      Py_XDECREF(arg);
+      if (!v) {
+        PyErr_Clear();  // the reference raises here: the Python plan reproduces it
+      } else if (PyDict_CheckExact(v) && PyDict_GET_SIZE(v) > 0) {
+        nym = v;
+      } else {
+        Py_DECREF(v);
+      }
+    }
+    Py_DECREF(data);
+    if (nym) {
+      const int rc = PyDict_SetItem(out, idr, nym);
+      Py_DECREF(nym);
+      if (rc < 0) goto fail;
+    }
+  }
+  Py_DECREF(seen);
+  Py_DECREF(seq);
+  return out;
+fail:
+  Py_DECREF(out);
+  Py_DECREF(seen);
+  Py_DECREF(seq);
+  return nullptr;
+}
+
 // ------------------------------------------------- request digests (f-3)
 // request_digests(reqs, sha_addr, device_mask) -> list of hex str or None
 // Request.getDigest() (plenum/common/request.py:71-72) for each request dict:
@@ -1105,6 +1319,8 @@ PyMethodDef kMethods[] = {
     {"auth_core_batch", py_auth_core_batch, METH_VARARGS,
      "whole-batch CoreAuthNr fast path with the GPU verify inside: (out, slow, rejected)"},
     {"last_phases", py_last_phases, METH_NOARGS, "phase seconds of the last auth_core_batch call"},
+    {"state_nyms", py_state_nyms, METH_VARARGS,
+     "NYMs of the identifiers getVerkey reads from the uncommitted state: {identifier: nym dict}"},
     {"auth_core_submit", py_auth_core_submit, METH_VARARGS,
      "asynchronous auth_core_batch (+ Request digests): queue the device call, return a handle"},
     {"auth_core_finish", py_auth_core_finish, METH_O,

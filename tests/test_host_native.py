@@ -520,3 +520,50 @@ def test_async_submit_finish_equals_sequential_with_digests(monkeypatch, with_st
     import gc as _gc
     _gc.collect()
     assert len(issued) == n_before + 1 and issued[-1] is True
+
+
+def test_native_state_nyms_equals_restatement():
+    """_edvhost.state_nyms (CPU SHA-256 state keys, the flat-JSON fast read,
+    json.loads for everything else) against the Python restatement
+    (CoreAuthNr._state_nyms_py) on the values a state can hold: plain objects,
+    duplicate keys, escapes, nesting, numbers of every JSON form, non-JSON
+    (NaN, trailing garbage, single quotes), non-ASCII, invalid UTF-8, str and
+    bytearray values, empty and falsy values, and clients entries that are
+    present, empty or falsy."""
+    import json
+    from indy_plenum_amd.client_authn import CoreAuthNr, nym_to_state_key
+    values = [
+        b'{"verkey": "~abc", "role": null}', b'{"verkey":"~a","verkey":"~b"}', b'{"verkey":"~a","verkey":null}',
+        b'{"verkey": null}', b'{"role": "0"}', b'{}', b' { "verkey" : "Full32ByteKeyXXXXXXXXXXXXXXXXXXXXX" } \n',
+        b'{"verkey":"~a","seqNo":12,"txnTime":1.5e9,"x":-0.25E-3,"t":true,"f":false}',
+        b'{"verkey":"~a","n":01}', b'{"verkey":"~a","n":1.}', b'{"verkey":"~a","n":NaN}', b'{"verkey":"~a"} x',
+        b"{'verkey':'~a'}", b'{"verk\\u0065y":"~esc"}', b'{"verkey":"~a\\n"}', b'{"verkey":"~a","o":{"k":1}}',
+        b'{"verkey":"~a","l":[1,2]}', '{"verkey":"~ünï"}'.encode(), b'{"verkey":"\xff"}', b'[1,2]', b'"str"',
+        b'', None, '{"verkey":"~strval"}', bytearray(b'{"verkey":"~ba"}'), b'{"verkey":"~a",}', b'{,}',
+        b'{"verkey":"~tab\there"}', b'  ', b'{"verkey":"~a"}\x00',
+    ]
+    st = _RecordingState()
+    reqs, clients = [], {}
+    for k, v in enumerate(values):
+        idr = "Idr%02d" % k
+        if v is not None:
+            st.kv[nym_to_state_key(idr)] = v
+        reqs.append({"identifier": idr, "reqId": k})
+    clients["Idr00"] = {"verkey": "~inmem"}          # answered from the clients map: no state read
+    clients["Idr01"] = {}                              # falsy: the state decides
+    clients["Idr02"] = None
+    reqs += [{"identifier": "Idr03"}, "notadict", {"identifier": ""}, {"identifier": 5}, {"reqId": 1}]
+    auth = CoreAuthNr(state=st)
+    auth.clients = clients
+    py = auth._state_nyms_py(reqs) or {}
+    reads_py = list(st.reads)
+    st.reads.clear()
+    nat = auth._state_nyms(reqs) or {}
+    assert st.reads == reads_py and not any(st.reads)  # the same reads, uncommitted, deduplicated
+
+    def view(d):
+        return {i: v.get("verkey") for i, v in d.items() if isinstance(v.get("verkey"), str)}
+    assert view(nat) == view(py)
+    assert set(nat) <= set(py)
+    assert view(py)["Idr06"] == "Full32ByteKeyXXXXXXXXXXXXXXXXXXXXX" and view(py)["Idr01"] == "~b"
+    assert "Idr00" not in py and "Idr13" in view(py)   # escaped key: json.loads path
