@@ -26,12 +26,41 @@
 #include <vector>
 #include <string>
 
+#ifdef EDV_STAMPS
+#define EDV_STAMP(slot) edv_main_stamp_fwd(slot)
+__device__ void edv_main_stamp_fwd(int slot);
+#endif
 #include "edv_verify_core.h"
 #include "edv_kernels.h"
 #include "edv_sha256.h"
 #include "../../include/edv.h"
 
 using namespace edv;
+
+#ifdef EDV_STAMPS
+// Diagnostic build only (tools/stamps.py): see edv_prep.hip.
+__device__ unsigned long long* g_main_stamps;
+__device__ __forceinline__ void edv_main_stamp(int slot) {
+  __builtin_amdgcn_sched_barrier(0);
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  if ((threadIdx.x & 63) == 0 && g_main_stamps) {
+    const unsigned wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    g_main_stamps[16ull * wave + slot] = t;
+  }
+}
+#define MAIN_STAMP(slot) edv_main_stamp(slot)
+__device__ void edv_main_stamp_fwd(int slot) { edv_main_stamp(slot); }
+namespace edv { hipError_t set_prep_stamps(void* buf); }
+extern "C" int edv_debug_set_stamps(void* prep_buf, void* main_buf) {
+  unsigned long long* p = static_cast<unsigned long long*>(main_buf);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_main_stamps), &p, sizeof p) != hipSuccess) return -3;
+  return edv::set_prep_stamps(prep_buf) == hipSuccess ? 0 : -3;
+}
+#else
+#define MAIN_STAMP(slot) ((void)0)
+#endif
 
 namespace {
 
@@ -103,6 +132,7 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
 #ifdef EDV_AB_SIDES  // prep-only measurement variant: the prep state is incomplete, so do nothing here
   return;
 #endif
+  MAIN_STAMP(0);
   const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
   const bool live = j < a.n && a.st.alive[j] && a.st.alive[a.st.cap + j] && a.st.alive[2 * a.st.cap + j];
   const uint32_t* d = a.st.dig + j;
@@ -138,7 +168,9 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   const int lane = int(threadIdx.x & 63);
   LdsATab at{a.st.atab + j * kAWords, wl, lane}, rt{a.st.rtab + j * kAWords, wl + kLdsAWords, lane};
   LdsBTab bt{a.btab, wl + 2 * kLdsAWords, lane};
+  MAIN_STAMP(1);
   a.accept[i] = main_one(da, db, bw, nwin, (wf >> 8) & 1, at, rt, bt) ? 1 : 0;
+  MAIN_STAMP(15);
 }
 
 // Comb rows for the batch signer, in global memory (528 KB, L2-resident).

@@ -39,6 +39,11 @@ namespace edv {
 #ifndef EDV_AWIN
 #define EDV_AWIN 4
 #endif
+// Phase stamps of the diagnostic build (EDV_STAMPS, tools/stamps.py): a no-op
+// everywhere else, the real kernels and the CPU build included.
+#ifndef EDV_STAMP
+#define EDV_STAMP(slot) ((void)0)
+#endif
 static_assert(EDV_AWIN == 4 || EDV_AWIN == 5, "window width 4 or 5");
 constexpr int kAWin = EDV_AWIN;                 // bits per [a](-A) / [b](-R) window
 constexpr int kAWindows = (255 + kAWin - 1) / kAWin;  // at most: 64 x 4 = 256 (51 x 5 = 255) bits >= 253
@@ -618,11 +623,15 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
   // hash and lattice first, points after: the two decompressions and tables
   // then run one after the other with little else live (register pressure)
   uint32_t dig[16], h[8];
+  EDV_STAMP(1);
   hram(dig, R, A, m, mlen);
+  EDV_STAMP(2);
   sc_reduce(h, dig);
+  EDV_STAMP(3);
   uint32_t a[8], u[8];
   bool neg;
   half_scalars(h, a, u, neg);
+  EDV_STAMP(4);
   // B scalar: b S mod L with b = (neg ? -u : u)
   uint32_t s[8];
   sc_mul(s, u, S);
@@ -636,6 +645,7 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
 #pragma unroll
     for (int i = 0; i < 8; i++) s[i] = t[i];
   }
+  EDV_STAMP(5);
   recode_bscalar(pd.bw, s);
   recode5(pd.da, a);
   recode5(pd.db, u);
@@ -654,8 +664,11 @@ template <class ATab>
 EDV_HD bool prep_point(const uint32_t P[8], ATab& tab) {
   if (!ge_is_canonical(P) || has_small_order(P)) return false;
   ge_p3 nP;
+  EDV_STAMP(1);
   if (!ge_frombytes_negate(nP, P)) return false;
+  EDV_STAMP(2);
   build_table(tab, nP);
+  EDV_STAMP(3);
   return true;
 }
 
@@ -717,7 +730,11 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
       t = ge_madd(p3, ge_precomp_cneg(bt.fetch(1), d1 < 0));
     }
     acc = ge_p1p1_to_p2(t);
+    if (w == nwin - 1) EDV_STAMP(2);         // after the top window (no doublings)
+    if (w == nwin - 5) EDV_STAMP(3);         // four windows later
+    if (w == 1) EDV_STAMP(4);                // before the last window
   }
+  EDV_STAMP(14);
   // identity: X = 0 and Y = Z (mod p)
   return fe_iszero(acc.X) && fe_iszero(fe_carry32(fe_sub(acc.Y, acc.Z)));
 }
