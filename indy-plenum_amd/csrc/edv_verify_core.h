@@ -714,6 +714,12 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
       bt.stage(0, d0 < 0 ? -d0 : d0);
       bt.stage(1, d1 < 0 ? -d1 : d1);
     }
+    // diagnostic stamps (EDV_STAMPS builds only): the phases of one plain
+    // window (slots 5-10) and of the B window w = 8 (slots 11-13); the LDS
+    // picks (fetch) are memory operations, so their waits stay in place, while
+    // pure arithmetic may drift across a stamp
+    const bool sw = w == nwin - 6, sb = w == 8;
+    if (sw) EDV_STAMP(5);
     ge_p3 p3;
     if (w == nwin - 1) {
       p3 = ge_p3_identity();
@@ -722,14 +728,24 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
       for (int d = 0; d < kAWin - 1; d++) acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
       p3 = ge_p1p1_to_p3(ge_p2_dbl(acc));
     }
-    p3 = ge_p1p1_to_p3(ge_add(p3, ge_cached_cneg(at.fetch(), dA < 0)));
-    ge_p1p1 t = ge_add(p3, ge_cached_cneg(rt.fetch(), (dR < 0) != negR));
+    if (sw) EDV_STAMP(6);
+    if (sb) EDV_STAMP(11);
+    const ge_cached ea = at.fetch();
+    if (sw) EDV_STAMP(7);
+    p3 = ge_p1p1_to_p3(ge_add(p3, ge_cached_cneg(ea, dA < 0)));
+    if (sw) EDV_STAMP(8);
+    const ge_cached er = rt.fetch();
+    if (sw) EDV_STAMP(9);
+    ge_p1p1 t = ge_add(p3, ge_cached_cneg(er, (dR < 0) != negR));
+    if (sb) EDV_STAMP(12);
     if (addB) {
       p3 = ge_p1p1_to_p3(t);
       p3 = ge_p1p1_to_p3(ge_madd(p3, ge_precomp_cneg(bt.fetch(0), d0 < 0)));
       t = ge_madd(p3, ge_precomp_cneg(bt.fetch(1), d1 < 0));
     }
     acc = ge_p1p1_to_p2(t);
+    if (sw) EDV_STAMP(10);
+    if (sb) EDV_STAMP(13);
     if (w == nwin - 1) EDV_STAMP(2);         // after the top window (no doublings)
     if (w == nwin - 5) EDV_STAMP(3);         // four windows later
     if (w == 1) EDV_STAMP(4);                // before the last window

@@ -63,4 +63,13 @@ out["main"] = {"prologue_cycles_p50": float(np.median(pro)), "top_window_cycles_
                "start_spread_p99": float(np.percentile(sm[:, 0] - m0, 99)),
                "end_p50": float(np.median(sm[:, 15] - m0)), "end_max": float((sm[:, 15] - m0).max()),
                "prologue_share": float(np.median(pro) / np.median(sm[:, 15] - sm[:, 0]))}
+win = sm[:, 10] - sm[:, 5]
+names = ["doublings", "fetch_A (LDS wait)", "add_A + to_p3", "fetch_R (LDS wait)", "add_R + to_p2"]
+d = np.diff(sm[:, 5:11], axis=1)
+out["main"]["plain_window"] = {"cycles_p50": float(np.median(win)),
+                               "shares": {nm: float(np.median(d[:, k]) / np.median(win)) for k, nm in enumerate(names)}}
+bw = sm[:, 13] - sm[:, 11]
+out["main"]["b_window_after_doublings"] = {"add_A_R_cycles_p50": float(np.median(sm[:, 12] - sm[:, 11])),
+                                          "b_adds_cycles_p50": float(np.median(sm[:, 13] - sm[:, 12])),
+                                          "cycles_p50": float(np.median(bw))}
 print(json.dumps(out, indent=1))

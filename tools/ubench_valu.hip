@@ -23,9 +23,9 @@ static const char* kNames[] = {"v_add_u32", "v_mad_u64_u32", "v_mul_lo_u32", "v_
 static const int kInstrPerStep[] = {1,1,1,1,1,1,1,2,1,1,1,1,1,1,1,1,1,2,1,1,1,1,1,1};
 
 constexpr int ITERS = 4096;   // loop trips
-constexpr int UNR = 8;       // chains per lane (independent)
+constexpr int UNR_MAX = 8;   // chains per lane (independent)
 
-template <int OP>
+template <int OP, int UNR = UNR_MAX>
 __global__ __launch_bounds__(256) void kbench(uint32_t* out, uint32_t seed) {
   uint32_t x = seed ^ threadIdx.x, y = seed * 3u + blockIdx.x;
   uint32_t r[UNR];
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void kbench(uint32_t* out, uint32_t seed) {
         if constexpr (OP == DOT2) asm volatile("v_dot2_u32_u16 %0, %1, %2, %0" : "+v"(r[i]) : "v"(x), "v"(y));
         if constexpr (OP == ALIGNBIT) asm volatile("v_alignbit_b32 %0, %0, %1, 13" : "+v"(r[i]) : "v"(x));
         if constexpr (OP == ADD3) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(r[i]) : "v"(x), "v"(y));
-        if constexpr (OP == LSHLADD64) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(q[i]) : "v"(q[(i + 1) % UNR]));
+        if constexpr (OP == LSHLADD64) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(q[i]) : "v"(dx));
         if constexpr (OP == FMA32) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(f[i]) : "v"(fx), "v"(fy));
         if constexpr (OP == BFI) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(r[i]) : "v"(x), "v"(y));
         if constexpr (OP == XOR) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(r[i]) : "v"(x));
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void kbench(uint32_t* out, uint32_t seed) {
         if constexpr (OP == ADDCO3) asm volatile("v_add_co_u32 %0, s[0:1], %0, %1" : "+v"(r[i]) : "v"(x) : "s0", "s1");
         if constexpr (OP == MADMIX) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0\n\tv_add_u32 %3, %3, %1" : "+v"(q[i]), "+v"(r[i]) : "v"(x), "v"(y) : "vcc");
         if constexpr (OP == LSHR) asm volatile("v_lshrrev_b32 %0, 7, %0" : "+v"(r[i]));
-        if constexpr (OP == ASHR64) asm volatile("v_ashrrev_i64 %0, 26, %1" : "=v"(q[i]) : "v"(q[(i + 1) % UNR]));
+        if constexpr (OP == ASHR64) asm volatile("v_ashrrev_i64 %0, 26, %0" : "+v"(q[i]));
         if constexpr (OP == MADI64) asm volatile("v_mad_i64_i32 %0, vcc, %1, %2, %0" : "+v"(q[i]) : "v"(x), "v"(y) : "vcc");
         if constexpr (OP == BITOP3) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x6c" : "+v"(r[i]) : "v"(x), "v"(y));
         if constexpr (OP == CND64) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(r[i]) : "v"(x), "s"(mask));
@@ -84,17 +84,20 @@ __global__ void kclock(unsigned long long* out, int spin) {
   if (threadIdx.x == 0 && blockIdx.x == 0) { out[0] = t1 - t0; out[1] = r1 - r0; out[2] = x; }
 }
 
-template <int OP>
-static void run(int ncu, uint32_t* dout, double clk_ghz) {
-  const int blocks = ncu * 8;  // 8 x 256 threads per CU = 8 waves/SIMD
+// wps waves per SIMD (blocks of 256 threads: one wave per SIMD each), UNR
+// independent chains per lane: wps 8 / UNR 8 is throughput, wps 1 is what one
+// wave alone sustains (the main kernel's regime), UNR 1 the dependent latency.
+template <int OP, int UNR = UNR_MAX>
+static void run(int ncu, uint32_t* dout, double clk_ghz, int wps = 8) {
+  const int blocks = ncu * wps;
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a)); CHECK(hipEventCreate(&b));
-  kbench<OP><<<blocks, 256>>>(dout, 1);  // warm-up
+  kbench<OP, UNR><<<blocks, 256>>>(dout, 1);  // warm-up
   CHECK(hipDeviceSynchronize());
   float best = 1e30f;
   for (int rep = 0; rep < 5; rep++) {
     CHECK(hipEventRecord(a));
-    kbench<OP><<<blocks, 256>>>(dout, rep + 2);
+    kbench<OP, UNR><<<blocks, 256>>>(dout, rep + 2);
     CHECK(hipEventRecord(b));
     CHECK(hipEventSynchronize(b));
     float ms; CHECK(hipEventElapsedTime(&ms, a, b));
@@ -104,8 +107,9 @@ static void run(int ncu, uint32_t* dout, double clk_ghz) {
   double per_simd = wave_instr / (ncu * 4.0);
   double cycles = best * 1e-3 * clk_ghz * 1e9;
   double lane_ops = wave_instr * 64 / (best * 1e-3);
-  printf("{\"op\": \"%s\", \"ms\": %.4f, \"cyc_per_wave_instr_per_simd\": %.3f, \"lane_Gops\": %.1f}\n",
-         kNames[OP], best, cycles / per_simd, lane_ops / 1e9);
+  printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"chains\": %d, \"ms\": %.4f, "
+         "\"cyc_per_wave_instr_per_simd\": %.3f, \"cyc_per_instr_per_wave\": %.3f, \"lane_Gops\": %.1f}\n",
+         kNames[OP], wps, UNR, best, cycles / per_simd, cycles / per_simd * wps, lane_ops / 1e9);
   CHECK(hipEventDestroy(a)); CHECK(hipEventDestroy(b));
 }
 
@@ -130,5 +134,13 @@ int main() {
   run<FMA32>(ncu, dout, ghz); run<BFI>(ncu, dout, ghz);
   run<XOR>(ncu, dout, ghz); run<CNDMASK>(ncu, dout, ghz); run<ADDCO3>(ncu, dout, ghz); run<MADMIX>(ncu, dout, ghz); run<LSHR>(ncu, dout, ghz);
   run<ASHR64>(ncu, dout, ghz); run<MADI64>(ncu, dout, ghz); run<BITOP3>(ncu, dout, ghz); run<CND64>(ncu, dout, ghz); run<MULI24>(ncu, dout, ghz);
+  // one wave per SIMD (the main kernel at 64k), and dependent chains (latency)
+  for (int wps : {1, 2}) {
+    run<MADI64>(ncu, dout, ghz, wps); run<ADD>(ncu, dout, ghz, wps); run<ASHR64>(ncu, dout, ghz, wps);
+    run<LSHLADD64>(ncu, dout, ghz, wps); run<MULLO>(ncu, dout, ghz, wps); run<MADMIX>(ncu, dout, ghz, wps);
+  }
+  run<MADI64, 1>(ncu, dout, ghz, 1); run<MADI64, 2>(ncu, dout, ghz, 1); run<MADI64, 4>(ncu, dout, ghz, 1);
+  run<ADD, 1>(ncu, dout, ghz, 1); run<ASHR64, 1>(ncu, dout, ghz, 1); run<LSHLADD64, 1>(ncu, dout, ghz, 1);
+  run<MULLO, 1>(ncu, dout, ghz, 1);
   return 0;
 }
