@@ -716,22 +716,23 @@ int digest_is_signing_bytes(PyObject* req) {
   Py_ssize_t pos = 0;
   PyObject *k, *v;
   int have = 0;
+  auto is = [](PyObject* key, PyObject* interned, const char* text) {
+    return key == interned || PyUnicode_CompareWithASCIIString(key, text) == 0;
+  };
   while (PyDict_Next(req, &pos, &k, &v)) {
+    // keys of a JSON-decoded request are equal to, not the same objects as, the
+    // interned names: compare by value when identity fails
     if (!PyUnicode_CheckExact(k)) return 0;
-    if (k == g_k_signature || k == g_k_signatures || k == g_k_fees) continue;
-    if (k == g_k_identifier || k == g_k_operation || k == g_k_reqid) { have++; continue; }
-    if (k == g_k_protocol) {
+    if (is(k, g_k_signature, "signature") || is(k, g_k_signatures, "signatures") || is(k, g_k_fees, "fees")) continue;
+    if (is(k, g_k_identifier, "identifier") || is(k, g_k_operation, "operation") || is(k, g_k_reqid, "reqId")) {
+      have++;
+      continue;
+    }
+    if (is(k, g_k_protocol, "protocolVersion")) {
       if (v == Py_None) return 0;
       continue;
     }
-    // a key equal to one of ours but not the interned object: compare by value
-    for (PyObject* kk : {g_k_signature, g_k_signatures, g_k_fees, g_k_identifier, g_k_operation, g_k_reqid,
-                         g_k_protocol}) {
-      const int eq = PyUnicode_Compare(k, kk);
-      if (eq == -1 && PyErr_Occurred()) return -1;
-      if (eq == 0) return 0;  // unusual key object: leave it to the general digest path
-    }
-    return 0;
+    return 0;  // any other key is in the signing bytes but not in signingState
   }
   return have == 3 ? 1 : 0;
 }

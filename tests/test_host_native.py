@@ -474,6 +474,8 @@ def test_async_submit_finish_equals_sequential_with_digests(monkeypatch, with_st
     monkeypatch.setattr(edv, "open_batch", counting_open)
     norm = lambda res: [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x)
                         for x in res]
+    if with_state:  # requests as the Node sees them: decoded from JSON, keys not interned
+        reqs = [json.loads(json.dumps(q)) if isinstance(q, dict) else q for q in reqs]
     p = sa.authenticate_batch_submit(reqs, digests=True)
     assert len(calls) == 1 and calls[0][1] and issued == [False]   # queued, not waited for
     assert norm(p.result()) == want and issued == [True]
