@@ -583,7 +583,7 @@ inline bool ascii_str(PyObject* o, const uint8_t** p, size_t* n) {
 
 // phase A for one request: false = not the fast path (nothing appended)
 PyObject *g_k_identifier, *g_k_signature, *g_k_verkey;  // interned key strings (module init)
-PyObject *g_k_reqid, *g_k_operation, *g_k_protocol;
+PyObject *g_k_reqid, *g_k_operation, *g_k_protocol, *g_k_type;
 
 // verkey source of one identifier, as SimpleAuthNr.getVerkey (client_authn.py:148-160)
 // reads it: the in-memory `clients` entry unless it is falsy, else the NYM the
@@ -695,6 +695,13 @@ struct Batch {
   size_t o_pk = 0, o_off = 0, o_msg = 0, o_acc = 0, o_dig = 0;
   Py_ssize_t n = 0;
   bool want_dig = false;
+  // ReqAuthenticator mode (req_auth_submit): the batch's requests are todo[] of
+  // n_all, kind[k] per request: 0 query, 1 no authenticator, 2 authenticated
+  // here, 3 left to the general Python path
+  bool req_mode = false;
+  Py_ssize_t n_all = 0;
+  std::vector<uint8_t> kind;
+  std::vector<Py_ssize_t> todo;
   // asynchronous submission (auth_core_submit): the batch is in flight until waited for
   bool pending = false;
   int device = 0;
@@ -997,6 +1004,209 @@ PyObject* py_auth_core_finish(PyObject*, PyObject* cap) {
     }
   }
   return build_output(*b, b->want_dig);
+}
+
+// ---- ReqAuthenticator.authenticate_batch_submit for the single stock
+// CoreAuthNr (req_authenticator.py:22-44 per request): the txn-type routing too.
+// req_auth_submit(reqs, clients, excluded, submit_addr, wait_addr, device, threads,
+//                 resolved, want_digests, (query_types, write_types, action_types))
+//   -> handle; kinds from req.get('operation', {}).get('type') against the three
+//   type sets, exactly as the reference evaluates them; a request whose type
+//   cannot be read that way (not a plain dict, an operation that is not a plain
+//   dict, an unhashable type) is left to the general Python path.
+// req_auth_finish(handle, NoAuthenticatorFound, InsufficientCorrectSignatures)
+//   -> (out, slow, general, digests or None): out[k] is the set ReqAuthenticator
+//   returns or the exception instance it raises; slow: requests the CoreAuthNr
+//   Python plan must finish (its result r becomes r if an exception, else
+//   set(r) or NoAuthenticatorFound()); general: requests for the general path.
+PyObject* py_req_auth_submit(PyObject*, PyObject* args) {
+  PyObject *reqs, *clients, *excluded, *resolved, *types;
+  unsigned long long saddr, waddr;
+  int device, threads, want;
+  if (!PyArg_ParseTuple(args, "OO!OKKiiOpO!", &reqs, &PyDict_Type, &clients, &excluded, &saddr, &waddr, &device,
+                        &threads, &resolved, &want, &PyTuple_Type, &types) || !parse_resolved(resolved))
+    return nullptr;
+  PyObject *qt, *wt, *at;
+  if (!PyArg_ParseTuple(types, "OOO", &qt, &wt, &at)) return nullptr;
+  PyObject* seq = PySequence_Fast(reqs, "req_auth_submit needs a sequence of requests");
+  if (!seq) return nullptr;
+  Batch* b = new Batch();
+  b->req_mode = true;
+  b->want_dig = want != 0;
+  b->device = device;
+  b->wait = reinterpret_cast<wait_fn_t>(uintptr_t(waddr));
+  PyObject* cap = PyCapsule_New(b, kBatchCapsule, batch_capsule_free);
+  if (!cap) { delete b; Py_DECREF(seq); return nullptr; }
+  b->n_all = PySequence_Fast_GET_SIZE(seq);
+  b->kind.assign(size_t(b->n_all), 3);
+  PyObject* sub = PyList_New(0);
+  if (!sub) { Py_DECREF(seq); Py_DECREF(cap); return nullptr; }
+  for (Py_ssize_t k = 0; k < b->n_all; k++) {
+    PyObject* req = PySequence_Fast_GET_ITEM(seq, k);
+    if (!PyDict_CheckExact(req)) continue;  // general path
+    PyObject* op = PyDict_GetItemWithError(req, g_k_operation);
+    if (!op && PyErr_Occurred()) goto fail;
+    PyObject* typ = Py_None;
+    if (op) {
+      if (!PyDict_CheckExact(op)) continue;
+      typ = PyDict_GetItemWithError(op, g_k_type);
+      if (!typ) {
+        if (PyErr_Occurred()) goto fail;
+        typ = Py_None;
+      }
+    }
+    Py_INCREF(typ);  // the contains() calls below may run Python code
+    int q = PySequence_Contains(qt, typ);
+    int kd = -1;
+    if (q > 0) kd = 0;
+    else if (q == 0) {
+      int w = PySequence_Contains(wt, typ);
+      if (w == 0) w = PySequence_Contains(at, typ);
+      if (w > 0) kd = 2;
+      else if (w == 0) kd = 1;
+    }
+    Py_DECREF(typ);
+    if (kd < 0) {
+      PyErr_Clear();  // an unhashable type: the general path raises what the reference raises
+      continue;
+    }
+    b->kind[size_t(k)] = uint8_t(kd);
+    if (kd == 2) {
+      b->todo.push_back(k);
+      if (PyList_Append(sub, req) < 0) goto fail;
+    }
+  }
+  Py_DECREF(seq);
+  if (collect_all(*b, sub, clients, resolved, excluded) < 0 || pack_all(*b, threads) < 0) {
+    Py_DECREF(sub);
+    Py_DECREF(cap);
+    return nullptr;
+  }
+  Py_DECREF(sub);
+  {
+    const size_t nf = b->items.size();
+    if (!nf) return cap;
+    const submit_fn_t submit = reinterpret_cast<submit_fn_t>(uintptr_t(saddr));
+    uint8_t* base = b->ar->p;
+    int64_t ticket = -1;
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = submit(base, base + b->o_pk, base + b->o_msg, reinterpret_cast<const uint64_t*>(base + b->o_off),
+                uint64_t(nf), base + b->o_acc, b->want_dig ? base + b->o_dig : nullptr, device, &ticket);
+    Py_END_ALLOW_THREADS
+    if (rc != 0) {
+      Py_DECREF(cap);
+      PyErr_Format(PyExc_RuntimeError, "edv_verify_digest_batch_async failed (%d)", rc);
+      return nullptr;
+    }
+    b->ticket = ticket;
+    b->pending = true;
+  }
+  return cap;
+fail:
+  Py_DECREF(sub);
+  Py_DECREF(seq);
+  Py_DECREF(cap);
+  return nullptr;
+}
+
+PyObject* py_req_auth_finish(PyObject*, PyObject* args) {
+  PyObject *cap, *no_auth, *ics;
+  if (!PyArg_ParseTuple(args, "OOO", &cap, &no_auth, &ics)) return nullptr;
+  Batch* b = static_cast<Batch*>(PyCapsule_GetPointer(cap, kBatchCapsule));
+  if (!b) return nullptr;
+  if (!b->req_mode) {
+    PyErr_SetString(PyExc_TypeError, "not a req_auth_submit handle");
+    return nullptr;
+  }
+  if (b->pending) {
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = b->wait(b->device, b->ticket);
+    Py_END_ALLOW_THREADS
+    b->pending = false;
+    if (rc != 0) {
+      PyErr_Format(PyExc_RuntimeError, "edv_wait_async failed (%d)", rc);
+      return nullptr;
+    }
+  }
+  const size_t nf = b->items.size();
+  const uint8_t* acc = nf ? b->ar->p + b->o_acc : nullptr;
+  const int gc_was = PyGC_Disable();
+  PyObject *out = PyList_New(b->n_all), *slow = PyList_New(0), *general = PyList_New(0), *digs = nullptr;
+  PyObject* res = nullptr;
+  if (b->want_dig) digs = PyList_New(b->n_all);
+  if (!out || !slow || !general || (b->want_dig && !digs)) goto fail;
+  for (Py_ssize_t k = 0; k < b->n_all; k++) {
+    PyObject* v;
+    switch (b->kind[size_t(k)]) {
+      case 0: v = PySet_New(nullptr); break;                   // query: set()
+      case 1: v = PyObject_CallNoArgs(no_auth); break;         // NoAuthenticatorFound
+      case 3: {
+        PyObject* i = PyLong_FromSsize_t(k);
+        if (!i || PyList_Append(general, i) < 0) { Py_XDECREF(i); goto fail; }
+        Py_DECREF(i);
+      }  // fall through: placeholder None
+      default: Py_INCREF(Py_None); v = Py_None;
+    }
+    if (!v) goto fail;
+    PyList_SET_ITEM(out, k, v);
+    if (digs) {
+      Py_INCREF(Py_None);
+      PyList_SET_ITEM(digs, k, Py_None);
+    }
+  }
+  for (Py_ssize_t j : b->slow_idx) {  // collect-phase misses: CoreAuthNr's Python plan
+    PyObject* i = PyLong_FromSsize_t(b->todo[size_t(j)]);
+    if (!i || PyList_Append(slow, i) < 0) { Py_XDECREF(i); goto fail; }
+    Py_DECREF(i);
+  }
+  for (size_t i = 0; i < nf; i++) {
+    const FastItem& it = b->items[i];
+    const Py_ssize_t k = b->todo[size_t(it.k)];
+    if (digs && b->dig_ok[i]) {
+      static const char hexd[] = "0123456789abcdef";
+      const uint8_t* d = b->ar->p + b->o_dig + 32 * i;
+      char h[64];
+      for (int q = 0; q < 32; q++) {
+        h[2 * q] = hexd[d[q] >> 4];
+        h[2 * q + 1] = hexd[d[q] & 15];
+      }
+      PyObject* v = PyUnicode_FromStringAndSize(h, 64);
+      if (!v) goto fail;
+      PyObject* old = PyList_GET_ITEM(digs, k);
+      PyList_SET_ITEM(digs, k, v);
+      Py_DECREF(old);
+    }
+    PyObject* v = nullptr;
+    if (!b->good[i]) {
+      PyObject* ix = PyLong_FromSsize_t(k);
+      if (!ix || PyList_Append(slow, ix) < 0) { Py_XDECREF(ix); goto fail; }
+      Py_DECREF(ix);
+      continue;
+    } else if (acc[i]) {
+      v = PySet_New(nullptr);                                  // {identifier}
+      if (v && PySet_Add(v, it.idr) < 0) { Py_DECREF(v); v = nullptr; }
+    } else {
+      v = PyObject_CallFunction(ics, "ii", 0, 1);              // InsufficientCorrectSignatures(0, 1)
+    }
+    if (!v) goto fail;
+    PyObject* old = PyList_GET_ITEM(out, k);
+    PyList_SET_ITEM(out, k, v);
+    Py_DECREF(old);
+  }
+  if (PyList_Sort(slow) < 0) goto fail;
+  if (digs) res = Py_BuildValue("(NNNN)", out, slow, general, digs);
+  else res = Py_BuildValue("(NNNO)", out, slow, general, Py_None);
+  if (gc_was) PyGC_Enable();
+  return res;
+fail:
+  if (gc_was) PyGC_Enable();
+  Py_XDECREF(out);
+  Py_XDECREF(slow);
+  Py_XDECREF(general);
+  Py_XDECREF(digs);
+  return nullptr;
 }
 
 // ------------------------------------- state-backed verkeys (P5, rows f-1/f-3)
@@ -1324,6 +1534,10 @@ PyMethodDef kMethods[] = {
      "NYMs of the identifiers getVerkey reads from the uncommitted state: {identifier: nym dict}"},
     {"auth_core_submit", py_auth_core_submit, METH_VARARGS,
      "asynchronous auth_core_batch (+ Request digests): queue the device call, return a handle"},
+    {"req_auth_submit", py_req_auth_submit, METH_VARARGS,
+     "ReqAuthenticator.authenticate_batch_submit for the single stock CoreAuthNr: type routing + auth_core_submit"},
+    {"req_auth_finish", py_req_auth_finish, METH_VARARGS,
+     "wait for a req_auth_submit handle: (out, slow, general, digests or None)"},
     {"auth_core_finish", py_auth_core_finish, METH_O,
      "wait for an auth_core_submit handle: (out, slow, rejected, digests or None)"},
     {"set_host_allocator", py_set_host_allocator, METH_VARARGS,
@@ -1351,6 +1565,7 @@ PyMODINIT_FUNC PyInit__edvhost(void) {
   g_k_operation = PyUnicode_InternFromString("operation");
   g_k_protocol = PyUnicode_InternFromString("protocolVersion");
   g_k_signatures = PyUnicode_InternFromString("signatures");
+  g_k_type = PyUnicode_InternFromString("type");
   g_k_fees = PyUnicode_InternFromString("fees");
   if (!g_k_identifier || !g_k_signature || !g_k_verkey) return nullptr;
   return PyModule_Create(&kModule);

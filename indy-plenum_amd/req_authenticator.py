@@ -17,7 +17,7 @@ from typing import Optional
 
 from .client_authn import ClientAuthNr
 from .constants import OPERATION, TXN_TYPE
-from .exceptions import NoAuthenticatorFound
+from .exceptions import InsufficientCorrectSignatures, NoAuthenticatorFound
 
 
 _gc_lock = threading.Lock()
@@ -121,6 +121,9 @@ class ReqAuthenticator:
         hashed (None elsewhere).  Only the single stock authenticator submits
         asynchronously; any other set-up is authenticated at once."""
         from .client_authn import PendingAuth
+        native = self._native_submit(reqs, digests)
+        if native is not None:
+            return native
         plan = self._single_stock_plan(reqs)
         if plan is None or not hasattr(plan[0], "authenticate_batch_submit"):
             out = self.authenticate_batch(reqs)
@@ -138,6 +141,43 @@ class ReqAuthenticator:
             for k, d in zip(todo, p.digests()):
                 dig[k] = d
             return out, dig
+        return PendingAuth(finish)
+
+    def _native_submit(self, reqs, digests):
+        """The whole submission natively (_edvhost.req_auth_submit: the type
+        routing of authenticate() and CoreAuthNr's fast path, one queued device
+        call) for the usual node: one stock CoreAuthNr whose type predicates are
+        the stock ones.  None = not applicable."""
+        from .client_authn import CoreAuthMixin, PendingAuth, DidVerifier, _edvhost
+        from . import edv
+        if len(self._authenticators) != 1 or _edvhost is None:
+            return None
+        a = self._authenticators[0]
+        cls = type(a)
+        if not (isinstance(a, CoreAuthMixin) and a.batch_reads_only() and a._stock(DidVerifier)
+                and edv.native_batch_enabled()
+                and cls.is_query is CoreAuthMixin.is_query and cls.is_write is CoreAuthMixin.is_write
+                and getattr(cls.is_action, "__func__", None) is CoreAuthMixin.is_action.__func__
+                and cls.authenticate_batch_submit is CoreAuthMixin.authenticate_batch_submit):
+            return None
+        submit, wait = edv.async_addresses()
+        with gc_paused():
+            h = _edvhost.req_auth_submit(reqs, a.clients, a.excluded_from_signing, submit, wait, edv.BATCH_DEVICE,
+                                         edv.PREP_THREADS, a._state_nyms(reqs), digests,
+                                         (a.query_types, a.write_types, cls.action_types))
+
+        def finish():
+            with gc_paused():
+                out, slow, general, digs = _edvhost.req_auth_finish(h, NoAuthenticatorFound,
+                                                                   InsufficientCorrectSignatures)
+                if slow:
+                    res = a._batch_planned([reqs[k] for k in slow], [None] * len(slow), DidVerifier)
+                    for k, rv in zip(slow, res):
+                        out[k] = rv if isinstance(rv, BaseException) else (set(rv) if rv else NoAuthenticatorFound())
+                if general:
+                    for k, r in zip(general, self._authenticate_batch([reqs[k] for k in general])):
+                        out[k] = r
+            return out, (digs if digs is not None else [None] * len(reqs))
         return PendingAuth(finish)
 
     def _authenticate_batch(self, reqs):

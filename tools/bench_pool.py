@@ -78,7 +78,11 @@ def run(mode, clients, reqs):
         pool = Pool(factory(clients, CoreAuthNr), n=4, batched=True, digest_fn=digest.request_digests,
                     overlap=mode == "gpu_batched_overlap")
     elif mode == "no_verify_ceiling":
-        pool = Pool(factory(clients, FreeAuthNr), n=4, batched=True, digest_fn=digest.request_digests)
+        # verification AND request digests free: digests looked up in a table
+        # made before the run, so this is the harness's own ceiling
+        table = dict(zip((r["reqId"] for r in reqs), digest.request_digests(reqs)))
+        pool = Pool(factory(clients, FreeAuthNr), n=4, batched=True,
+                    digest_fn=lambda rs: [table[r["reqId"]] for r in rs])
     else:
         pool = Pool(factory(clients, sodium_ref.SodiumCoreAuthNr), n=4, batched=False, digest_fn=cpu_digests)
     native = base58._native
