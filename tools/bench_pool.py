@@ -61,6 +61,9 @@ class FreeAuthNr(CoreAuthNr):
     def authenticate_batch(self, reqs, verifier=None):
         return [[r["identifier"]] for r in reqs]
 
+    def batch_reads_only(self):
+        return True   # nothing is mutated: no per-request deepcopy in ReqAuthenticator
+
 
 def factory(clients, cls):
     def make(_name):
