@@ -27,6 +27,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -765,6 +768,58 @@ int collect_all(Batch& b, PyObject* seq, PyObject* clients, PyObject* resolved, 
   return 0;
 }
 
+// A persistent pool for phase B: a Node's prod batch is a few hundred
+// requests, for which starting threads per call would cost more than the
+// decoding they share.  Workers never touch Python objects (they read the
+// items' text, which the batch keeps referenced, and write the arena).
+struct DecodePool {
+  std::mutex mu;
+  std::condition_variable go, done;
+  int workers = 0, parts = 0, remaining = 0;
+  uint64_t gen = 0;
+  const std::function<void(int)>* job = nullptr;
+  void ensure(int k) {  // caller holds no lock; called with the GIL held (one caller at a time)
+    while (workers < k) {
+      const int id = workers++;
+      std::thread([this, id] { loop(id); }).detach();  // lives as long as the process
+    }
+  }
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        go.wait(lk, [&] { return gen != seen; });
+        seen = gen;
+        if (id + 1 >= parts) continue;
+        f = job;
+      }
+      (*f)(id + 1);
+      std::lock_guard<std::mutex> lk(mu);
+      if (--remaining == 0) done.notify_all();
+    }
+  }
+  // runs f(0..n-1): f(0) on the calling thread, the rest on workers
+  void run(int n, const std::function<void(int)>& f) {
+    if (n <= 1) { f(0); return; }
+    ensure(n - 1);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      job = &f;
+      parts = n;
+      remaining = n - 1;
+      gen++;
+    }
+    go.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> lk(mu);
+    done.wait(lk, [&] { return remaining == 0; });
+  }
+};
+DecodePool* g_pool = nullptr;  // never destroyed: detached workers wait on it until exit
+std::mutex g_pool_mu;          // one batch decodes at a time (the GIL is released meanwhile)
+
 // phase B: arena + base58 decoding on `threads` threads (releases the GIL)
 int pack_all(Batch& b, int threads) {
   const size_t nf = b.items.size();
@@ -782,9 +837,11 @@ int pack_all(Batch& b, int threads) {
     return -1;
   }
   uint8_t* base = b.ar->p;
+  if (!g_pool) g_pool = new DecodePool();
   Py_BEGIN_ALLOW_THREADS
-  const int T = nf < 2048 ? 1 : std::max(1, std::min(threads, 32));
-  auto part = [&](int t) {
+  // about 100 requests per part: a part costs tens of microseconds, a hand-off a few
+  const int T = std::max(1, std::min({threads, 32, int(nf / 96)}));
+  const std::function<void(int)> part = [&](int t) {
     const size_t lo = nf * size_t(t) / size_t(T), hi = nf * size_t(t + 1) / size_t(T);
     for (size_t i = lo; i < hi; i++)
       if (!decode_one(b.items[i], base + 64 * i, base + b.o_pk + 32 * i)) {
@@ -795,10 +852,10 @@ int pack_all(Batch& b, int threads) {
     const size_t mlo = b.msgs.size() * size_t(t) / size_t(T), mhi = b.msgs.size() * size_t(t + 1) / size_t(T);
     memcpy(base + b.o_msg + mlo, b.msgs.data() + mlo, mhi - mlo);
   };
-  std::vector<std::thread> th;
-  for (int t = 1; t < T; t++) th.emplace_back(part, t);
-  part(0);
-  for (auto& x : th) x.join();
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool->run(T, part);
+  }
   memcpy(base + b.o_off, b.moff.data(), 8 * (nf + 1));
   memset(base + b.o_msg + b.msgs.size(), 0, 64);
   Py_END_ALLOW_THREADS

@@ -25,6 +25,24 @@ _gc_depth = 0       # paused sections in progress, over all threads
 _gc_was = False     # GC state when the first of them began
 
 
+GC_PAUSE_MIN = 4096  # batches smaller than this leave the GC alone
+
+
+@contextmanager
+def gc_paused_for(n):
+    """gc_paused for a batch of n requests; nothing for a small one.  A large
+    batch makes tens of thousands of containers, whose allocations would
+    trigger repeated collections over every live object of the node; a Node
+    prod's batch (a few hundred requests) makes a few hundred, and pausing then
+    only moves a collection the node's own allocations triggered to the pause's
+    end, inside the batch call."""
+    if n < GC_PAUSE_MIN:
+        yield
+        return
+    with gc_paused():
+        yield
+
+
 @contextmanager
 def gc_paused():
     """Pause the cyclic GC while a batch makes one small container per request
@@ -161,13 +179,13 @@ class ReqAuthenticator:
                 and cls.authenticate_batch_submit is CoreAuthMixin.authenticate_batch_submit):
             return None
         submit, wait = edv.async_addresses()
-        with gc_paused():
+        with gc_paused_for(len(reqs)):
             h = _edvhost.req_auth_submit(reqs, a.clients, a.excluded_from_signing, submit, wait, edv.BATCH_DEVICE,
                                          edv.PREP_THREADS, a._state_nyms(reqs), digests,
                                          (a.query_types, a.write_types, cls.action_types))
 
         def finish():
-            with gc_paused():
+            with gc_paused_for(len(reqs)):
                 out, slow, general, digs = _edvhost.req_auth_finish(h, NoAuthenticatorFound,
                                                                    InsufficientCorrectSignatures)
                 if slow:
