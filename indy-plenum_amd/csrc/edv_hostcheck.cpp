@@ -34,6 +34,7 @@ struct HostBTab {
 struct HostBStage {
   const HostBTab& b;
   int j[kBTables] = {0, 0};
+  void issue() {}
   void stage(int t, int e) { j[t] = e; }
   ge_precomp fetch(int t) const { return b.entry(t, j[t]); }
 };

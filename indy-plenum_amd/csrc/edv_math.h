@@ -752,13 +752,60 @@ EDV_HD uint64_t rotr64(uint64_t x, int n) {
   return pack64(funnel32(p.hi, p.lo, n), funnel32(p.lo, p.hi, n));
 }
 
+// A 64-bit value the optimizer cannot look into: a pair packed from two 32-bit
+// halves is otherwise rewritten as zext(lo) + (hi << 32) and the two pieces are
+// added separately into the round's 64-bit sums (two v_lshl_add_u64 and a
+// v_mov_b32 more per use).
+EDV_HD uint64_t opaque_u64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
+// Three-input bitwise functions as one v_bitop3_b32 per 32-bit half (gfx950):
+// LLVM does not form bitop3 from the 64-bit expressions, which cost two
+// v_xor_b32 per half for a three-way xor and four ops per half for Maj.  Both
+// truth tables are symmetric in their inputs, so operand order cannot matter.
+EDV_HD uint32_t xor3_32(uint32_t x, uint32_t y, uint32_t z) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(x, y, z, 0x96);
+#else
+  return x ^ y ^ z;
+#endif
+}
+EDV_HD uint32_t maj32(uint32_t x, uint32_t y, uint32_t z) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(x, y, z, 0xE8);
+#else
+  return (x & y) ^ (x & z) ^ (y & z);
+#endif
+}
+EDV_HD uint64_t xor3_64(uint64_t x, uint64_t y, uint64_t z) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const u32x2 a = __builtin_bit_cast(u32x2, x), b = __builtin_bit_cast(u32x2, y), c = __builtin_bit_cast(u32x2, z);
+  return opaque_u64(pack64(__builtin_amdgcn_bitop3_b32(a.lo, b.lo, c.lo, 0x96),
+                           __builtin_amdgcn_bitop3_b32(a.hi, b.hi, c.hi, 0x96)));
+#else
+  return x ^ y ^ z;
+#endif
+}
+EDV_HD uint64_t maj64(uint64_t x, uint64_t y, uint64_t z) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const u32x2 a = __builtin_bit_cast(u32x2, x), b = __builtin_bit_cast(u32x2, y), c = __builtin_bit_cast(u32x2, z);
+  return opaque_u64(pack64(__builtin_amdgcn_bitop3_b32(a.lo, b.lo, c.lo, 0xE8),
+                           __builtin_amdgcn_bitop3_b32(a.hi, b.hi, c.hi, 0xE8)));
+#else
+  return (x & y) ^ (x & z) ^ (y & z);
+#endif
+}
+
 EDV_HD void sha512_round(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t& e, uint64_t& f, uint64_t& g,
                          uint64_t& h, uint64_t kw) {
-  const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+  const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
   const uint64_t ch = (e & f) ^ (~e & g);
   const uint64_t t1 = h + S1 + ch + kw;
-  const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-  const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+  const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
+  const uint64_t mj = maj64(a, b, c);
   d += t1;
   h = t1 + S0 + mj;
 }
@@ -794,8 +841,8 @@ EDV_HD void sha512_compress(uint64_t H[8], uint64_t W[16]) {
 #pragma unroll
       for (int t = 0; t < 16; t++) {
         const uint64_t w15 = W[(t + 1) & 15], w2 = W[(t + 14) & 15];
-        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+        const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), opaque_u64(w15 >> 7));
+        const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), opaque_u64(w2 >> 6));
         W[t] += s0 + W[(t + 9) & 15] + s1;
       }
     }

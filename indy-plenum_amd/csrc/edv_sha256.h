@@ -34,18 +34,18 @@ EDV_HD void sha256_compress(uint32_t H[8], uint32_t W[16]) {
 #pragma unroll
       for (int t = 0; t < 16; t++) {
         const uint32_t w15 = W[(t + 1) & 15], w2 = W[(t + 14) & 15];
-        const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-        const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+        const uint32_t s0 = xor3_32(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+        const uint32_t s1 = xor3_32(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
         W[t] += s0 + W[(t + 9) & 15] + s1;
       }
     }
 #pragma unroll
     for (int t = 0; t < 16; t++) {
-      const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+      const uint32_t S1 = xor3_32(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
       const uint32_t ch = (e & f) ^ (~e & g);
       const uint32_t t1 = h + S1 + ch + K[r + t] + W[t];
-      const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
-      const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+      const uint32_t S0 = xor3_32(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+      const uint32_t mj = maj32(a, b, c);
       h = g; g = f; f = e; e = d + t1;
       d = c; c = b; b = a; a = t1 + S0 + mj;
     }

@@ -70,11 +70,21 @@ namespace {
 // (global_load_lds_dwordx4: 64 lanes x 16 B per instruction, lane-linear), so
 // nothing of it sits in registers during the window's doublings; fetch()
 // waits for the copies and reads the lane's 16-byte pieces back.  Per wave:
-// A 10 KiB + R 10 KiB + two B entries 8 KiB each = 36 KiB; 144 KiB per
-// 256-thread workgroup (one workgroup per CU at 64k signatures).
+// A 10 KiB + R 10 KiB = 20 KiB (80 KiB per 256-thread workgroup); the B
+// entries go to registers (RegBTab), or with EDV_MAIN_BLDS through LDS as well
+// (+16 KiB per wave, one workgroup per CU).
 constexpr int kLdsAWords = 10 * 256;  // one cached entry: 10 pieces of 64 lanes x 4 words
 constexpr int kLdsBWords = 8 * 256;   // one B entry: 8 pieces (words 30, 31 are padding)
+#ifndef EDV_MAIN_BLDS
+// B entries in registers (RegBTab below): the wave's LDS slice holds only the A
+// and R entries, 20 KiB, so two 256-thread workgroups fit a CU (2 waves/SIMD
+// once a chunk has more than one wave per SIMD: main 5.5 % faster at 2^18
+// signatures, the same at 2^16, profiles/r03/ab_main_s8.jsonl).  EDV_MAIN_BLDS
+// builds the round-2 layout (B entries staged through LDS too, 36 KiB/wave).
+constexpr int kLdsWaveWords = 2 * kLdsAWords;
+#else
 constexpr int kLdsWaveWords = 2 * kLdsAWords + kBTables * kLdsBWords;
+#endif
 __device__ __forceinline__ void wait_staged() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 struct LdsATab {
   const int32_t* slot;  // this lane's table in global memory
@@ -119,6 +129,33 @@ struct LdsBTab {
     for (int q = 0; q < 8; q++) {
       const int4 v = reinterpret_cast<const int4*>(lds + tb * kLdsBWords + q * 256)[lane];
       t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
+    }
+    return precomp_from_words(t);
+  }
+  __device__ __forceinline__ void issue() {}
+};
+// B entries straight into registers, loaded late in the window (issue() runs
+// after the R entry's LDS pick, so the loads fly during the R addition): no
+// LDS, at the price of 64 registers live across one addition every fourth
+// window.
+struct RegBTab {
+  const int32_t* w;
+  int j[kBTables];
+  int4 v[kBTables][8];
+  __device__ __forceinline__ void stage(int tb, int e) { j[tb] = e; }
+  __device__ __forceinline__ void issue() {
+#pragma unroll
+    for (int tb = 0; tb < kBTables; tb++) {
+      const int4* g = reinterpret_cast<const int4*>(w + (tb * kBEntries + j[tb]) * kBStride);
+#pragma unroll
+      for (int q = 0; q < 8; q++) v[tb][q] = g[q];
+    }
+  }
+  __device__ __forceinline__ ge_precomp fetch(int tb) {
+    int32_t t[32];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      t[4 * q] = v[tb][q].x; t[4 * q + 1] = v[tb][q].y; t[4 * q + 2] = v[tb][q].z; t[4 * q + 3] = v[tb][q].w;
     }
     return precomp_from_words(t);
   }
@@ -167,7 +204,11 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   int32_t* wl = lds_main + (threadIdx.x >> 6) * kLdsWaveWords;
   const int lane = int(threadIdx.x & 63);
   LdsATab at{a.st.atab + j * kAWords, wl, lane}, rt{a.st.rtab + j * kAWords, wl + kLdsAWords, lane};
+#ifndef EDV_MAIN_BLDS
+  RegBTab bt{a.btab, {0, 0}, {}};
+#else
   LdsBTab bt{a.btab, wl + 2 * kLdsAWords, lane};
+#endif
   MAIN_STAMP(1);
   a.accept[i] = main_one(da, db, bw, nwin, (wf >> 8) & 1, at, rt, bt) ? 1 : 0;
   MAIN_STAMP(15);

@@ -678,7 +678,8 @@ EDV_HD bool prep_point(const uint32_t P[8], ATab& tab) {
 // nwin: windows to walk (the wave's maximum; >= every lane's own count);
 // da/db are consumed from the top (shifted left 5 bits per window), bw from
 // entry kBDigits-1 down.  ATab provides stage(e) then fetch() -> cached entry e;
-// BTab stage(t, j) then fetch(t) -> entry j of table t.
+// BTab stage(t, j), issue() (after the R entry's pick: the register
+// variant starts its loads there) then fetch(t) -> entry j of table t.
 template <class ATab, class BTab>
 EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int nwin, bool negR, ATab& at, ATab& rt,
                      BTab& bt) {
@@ -735,6 +736,7 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
     p3 = ge_p1p1_to_p3(ge_add(p3, ge_cached_cneg(ea, dA < 0)));
     if (sw) EDV_STAMP(8);
     const ge_cached er = rt.fetch();
+    if (addB) bt.issue();
     if (sw) EDV_STAMP(9);
     ge_p1p1 t = ge_add(p3, ge_cached_cneg(er, (dR < 0) != negR));
     if (sb) EDV_STAMP(12);
