@@ -97,6 +97,16 @@ def kernel_source_hash():
     return h.hexdigest()
 
 
+# What the traffic figure is and why it stays: measured,
+# profiles/r03/pmc_extra_s10.json and bench_c3_full_s10.json.
+TRAFFIC_NOTE = ("L2-to-fabric bytes: the main kernel gathers one 160-B entry per window from each of two per-lane "
+                "1,440-B point tables the prep kernel wrote (~17.6 kB per verify; 2 x 128-B lines per entry), not "
+                "the 361 B of inputs. The counters cannot split Infinity-Cache hits from DRAM "
+                "(TCC_EA0_RDREQ_DRAM_sum == TCC_EA0_RDREQ_sum); at C2 the 189 MB of tables fit the 256 MiB "
+                "Infinity Cache, at 2^18 per launch (755 MB of tables, read from DRAM) the main kernel takes no "
+                "longer per verify, so the traffic is not what bounds it")
+
+
 def pmc_figures(kernels, batch, msg_len, kernel_ms):
     """Counter-derived figures for the verify path (`kernels`, summed) from the
     committed rocprofv3 PMC summary (tools/pmc_summary.py), only if it was
@@ -118,6 +128,8 @@ def pmc_figures(kernels, batch, msg_len, kernel_ms):
     for key in ("dram_bytes_per_launch_bound", "dram_note"):
         if key in s:
             out[key] = s[key]
+    out["traffic_per_verify_bytes"] = out["traffic"] / batch
+    out["traffic_note"] = TRAFFIC_NOTE
     cs = [k["counters"] for k in ks]
     if all("SQ_INSTS_VALU" in c for c in cs):
         valu = sum(c["SQ_INSTS_VALU"] for c in cs)  # wave-instructions per launch pair

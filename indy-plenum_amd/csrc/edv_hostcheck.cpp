@@ -68,6 +68,7 @@ void from_fe(int32_t* l, const fe& f) { for (int i = 0; i < 10; i++) l[i] = f.v[
 extern "C" {
 void hc_fe_mul(const int32_t* f, const int32_t* g, int32_t* h) { from_fe(h, fe_mul(to_fe(f), to_fe(g))); }
 void hc_fe_sq(const int32_t* f, int32_t* h) { from_fe(h, fe_sq(to_fe(f))); }
+void hc_fe_sq_floor(const int32_t* f, int32_t* h) { from_fe(h, fe_sq_floor(to_fe(f))); }
 void hc_fe_sq2(const int32_t* f, int32_t* h) { from_fe(h, fe_sq2(to_fe(f))); }
 void hc_fe_carry32(const int32_t* f, int32_t* h) { from_fe(h, fe_carry32(to_fe(f))); }
 void hc_fe_invert(const int32_t* f, int32_t* h) { from_fe(h, fe_invert(to_fe(f))); }
@@ -150,6 +151,8 @@ void hc_recode_bscalar(const uint8_t* s32, uint32_t* out9) {
   recode_bscalar(out9, s);
 }
 int hc_btab_entries() { return kBEntries; }
+// windows the packed radix-2^kAWin digits need (the prep kernel's per-lane count)
+int hc_digits_windows(const uint32_t* d8) { return digits5_windows(d8); }
 // packed signed digits of a 32-byte scalar at radix 2^bits: 4 (64 digits: the main
 // loop's windows at kAWin = 4), 5 (51 digits), 8 -> recode8 (signer), 15 / 16 -> the
 // generic recoder (17 / 16 digits)

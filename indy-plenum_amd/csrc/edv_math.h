@@ -109,10 +109,14 @@ EDV_HD fe fe_carry64(int64_t h0, int64_t h1, int64_t h2, int64_t h3, int64_t h4,
 // v_lshl_add_u64, 11.3k -> 10.7k instructions, 204 -> 193 VGPRs).
 EDV_HD constexpr int64_t col_bias(int k) { return (k & 1) ? (int64_t(1) << 24) : (int64_t(1) << 25); }
 #if defined(__HIP_DEVICE_COMPILE__)
-__constant__ int64_t c_col_bias[2] = {int64_t(1) << 25, int64_t(1) << 24};
+__constant__ int64_t c_col_bias[3] = {int64_t(1) << 25, int64_t(1) << 24, 0};
 EDV_HD int64_t bias_reg(int k) { return c_col_bias[k & 1]; }
+// an opaque zero addend: keeps an unbiased column's first product one
+// v_mad_i64_i32 (a literal 0 would make it a mul_lo/mul_hi pair)
+EDV_HD int64_t zero_reg() { return c_col_bias[2]; }
 #else
 EDV_HD int64_t bias_reg(int k) { return col_bias(k); }
+EDV_HD int64_t zero_reg() { return 0; }
 #endif
 template <int W>
 EDV_HD int32_t carry_biased(int64_t t, int64_t& next) {
@@ -224,7 +228,7 @@ constexpr sq_split kSqSplit[2][10][10] = {
         {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {2, 19}, {19, 4}},
         {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {19, 4}},
     }};
-template <bool DOUBLE>
+template <bool DOUBLE, bool BIAS = true>
 EDV_HD void fe_sq_cols(const fe& f, int64_t h[10]) {
   bool first[10];
 #pragma unroll
@@ -236,7 +240,7 @@ EDV_HD void fe_sq_cols(const fe& f, int64_t h[10]) {
       const int k = (i + j) % 10;
       const sq_split m = kSqSplit[DOUBLE ? 1 : 0][i][j];
       const int32_t a = f.v[i] * int32_t(m.x), b = f.v[j] * int32_t(m.y);
-      h[k] = first[k] ? int64_t(a) * int64_t(b) + bias_reg(k) : h[k] + int64_t(a) * int64_t(b);
+      h[k] = first[k] ? int64_t(a) * int64_t(b) + (BIAS ? bias_reg(k) : zero_reg()) : h[k] + int64_t(a) * int64_t(b);
       first[k] = false;
     }
   }
@@ -246,6 +250,41 @@ EDV_HD fe fe_sq(const fe& f) {
   int64_t h[10];
   fe_sq_cols<false>(f, h);
   const fe r = fe_carry64_biased(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
+  sched_fence();
+  return r;
+}
+// f^2 with floor carries (no rounding bias): limbs come out in [0, 2^26) /
+// [0, 2^25) (h1 within 2^16 of that range), one 32-bit subtraction per limb
+// cheaper than fe_sq.  Twice fe_sq's limb magnitude, so an output may feed
+// fe_sq / fe_sq_floor / fe_mul directly (inside their input bounds:
+// 19 x 2^26 and 38 x (2^25 + 2^16) < 2^31 for the premultiplied operands,
+// columns < 2^59), but not a sum or difference into a product.  Used for the
+// runs of squarings in the exponentiations (fe_sqn).
+template <int W>
+EDV_HD int32_t carry_floor(int64_t t, int64_t& next) {
+  next += t >> W;  // arithmetic shift: floor
+  return int32_t(uint32_t(t) & ((1u << W) - 1));
+}
+EDV_HD fe fe_sq_floor(const fe& f) {
+  sched_fence();
+  int64_t h[10];
+  fe_sq_cols<false, false>(f, h);
+  int64_t c9 = 0;
+  int32_t o[10];
+  o[0] = carry_floor<26>(h[0], h[1]);
+  o[1] = carry_floor<25>(h[1], h[2]);
+  o[2] = carry_floor<26>(h[2], h[3]);
+  o[3] = carry_floor<25>(h[3], h[4]);
+  o[4] = carry_floor<26>(h[4], h[5]);
+  o[5] = carry_floor<25>(h[5], h[6]);
+  o[6] = carry_floor<26>(h[6], h[7]);
+  o[7] = carry_floor<25>(h[7], h[8]);
+  o[8] = carry_floor<26>(h[8], h[9]);
+  o[9] = carry_floor<25>(h[9], c9);
+  int64_t t0 = int64_t(o[0]) + 19 * c9, t1 = o[1];
+  o[0] = carry_floor<26>(t0, t1);
+  o[1] = int32_t(t1);
+  const fe r{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8], o[9]}};
   sched_fence();
   return r;
 }
@@ -327,9 +366,12 @@ EDV_HD bool fe_isnegative(const fe& f) {
   return w[0] & 1;
 }
 
+#ifndef EDV_SQN_FLOOR
+#define EDV_SQN_FLOOR 1
+#endif
 EDV_HD fe fe_sqn(fe f, int n) {
 #pragma unroll 1
-  for (int i = 0; i < n; i++) f = fe_sq(f);
+  for (int i = 0; i < n; i++) f = EDV_SQN_FLOOR ? fe_sq_floor(f) : fe_sq(f);
   return f;
 }
 // z^(2^250 - 1) and z^11 (shared prefix of the inversion and sqrt chains)

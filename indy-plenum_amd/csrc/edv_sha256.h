@@ -63,11 +63,14 @@ EDV_HD void msg_words32_tail(uint32_t W[16], const uint8_t* m, uint64_t mlen, ui
   const uint32_t sh = uint32_t(a & 3);
   const uintptr_t base = a - sh;
   const uintptr_t last = (reinterpret_cast<uintptr_t>(m) + mlen) & ~uintptr_t(3);
+  const int32_t lim = int32_t(int64_t(last) - int64_t(base));  // < 0 for a block wholly past the end
   uint32_t d[17];
 #pragma unroll
   for (int t = 0; t < 17; t++) {
-    const uintptr_t ad = base + 4 * uintptr_t(t);
-    d[t] = *reinterpret_cast<const uint32_t*>(ad < last ? ad : last);
+    // min(base + 4t, last) as last - max(lim - 4t, 0): one v_max_i32 instead of
+    // a 64-bit compare and two VCC-mask selects
+    const int32_t back = lim - 4 * t;
+    d[t] = *reinterpret_cast<const uint32_t*>(last - uintptr_t(uint32_t(back > 0 ? back : 0)));
   }
   const int32_t rem0 = int32_t(int64_t(mlen) - int64_t(q0));
 #pragma unroll

@@ -397,6 +397,13 @@ constexpr int kQ = 4;
 // per prod in flight, and a pool of nodes in one process (C5) one per node, so
 // eight slots let up to eight callers overlap before a submission has to wait.
 constexpr int kAsyncSlots = 8;
+// An asynchronous batch of at most this many requests (a Node's prod carries a
+// few hundred) runs on its slot's own stream with its slot's own scratch
+// (~25 MB), so the small batches of several callers execute side by side on
+// the GPU instead of queueing behind each other on one stream: a batch that
+// small is one wave per SIMD on a few SIMDs, and its latency (one main-kernel
+// walk, ~0.45 ms) is all it costs.  Larger batches share the chunk scratch.
+constexpr uint64_t kSmallAsync = 8192;
 
 // One set of per-chunk state buffers (ChunkState storage + bucket permutation).
 struct ChunkBufs {
@@ -447,6 +454,8 @@ struct DevCtx {
     uint64_t n = 0;
     bool acc_pinned = false;     // verdicts DMA'd straight into `accept`
     bool dig_pinned = false;     // digests DMA'd straight into `digests`
+    hipStream_t st = nullptr;    // small batches: copies, kernels and D2H all on this stream
+    ChunkBufs cb;                // small batches: the slot's own chunk scratch (kSmallAsync)
   };
   AsyncSlot as[kAsyncSlots];
   hipStream_t hac = nullptr;
@@ -564,7 +573,7 @@ int phys_of(int device, int* phys) {
 
 VerifyArgs make_args(const DevCtx& c, ChunkBufs& b, const uint8_t* d_sigs, const uint8_t* d_pks,
                      const uint8_t* d_msgs, const uint64_t* d_off, uint64_t msg_base, uint8_t* d_accept, bool bucket,
-                     uint64_t slot0 = 0) {
+                     uint64_t slot0 = 0, uint64_t cap = 0) {
   VerifyArgs va;
   va.sigs = reinterpret_cast<const uint32_t*>(d_sigs);
   va.pks = reinterpret_cast<const uint32_t*>(d_pks);
@@ -575,7 +584,7 @@ VerifyArgs make_args(const DevCtx& c, ChunkBufs& b, const uint8_t* d_sigs, const
   // slots [slot0, slot0 + n) of the chunk scratch (dig stays indexed w * cap + slot)
   va.st = ChunkState{static_cast<int32_t*>(b.atab.p) + slot0 * kAWords, static_cast<int32_t*>(b.rtab.p) + slot0 * kAWords,
                      static_cast<uint32_t*>(b.dig.p) + slot0,
-                     static_cast<uint8_t*>(b.alive.p) + slot0, c.chunk,
+                     static_cast<uint8_t*>(b.alive.p) + slot0, cap ? cap : c.chunk,
                      bucket ? static_cast<uint32_t*>(b.perm.p) + slot0 : nullptr};
   va.btab = c.btab;
   va.base = 0;
@@ -634,6 +643,25 @@ int launch(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t
   return 0;
 }
 
+// A small asynchronous batch on its slot's own scratch (row stride cap) and
+// stream: no ordering against the shared scratch, so batches of different
+// slots run concurrently.  Chunks of at most c.chunk, as launch() walks them.
+int launch_own(DevCtx& c, ChunkBufs& cb, uint64_t cap, const uint8_t* d_sigs, const uint8_t* d_pks,
+               const uint8_t* d_msgs, const uint64_t* d_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept,
+               hipStream_t s, uint32_t flags) {
+  if (n == 0) return 0;
+  const bool bucket = bucketing_enabled(c, flags);
+  VerifyArgs va = make_args(c, cb, d_sigs, d_pks, d_msgs, d_off, msg_base, d_accept, bucket, 0, cap);
+  const uint64_t step = c.chunk < cap ? c.chunk : cap;
+  int err;
+  for (uint64_t base = 0; base < n; base += step) {
+    va.base = base;
+    va.n = (n - base) < step ? (n - base) : step;
+    if ((err = launch_prep(bucket_ctr(cb, 0), va, d_off, bucket, s)) || (err = launch_main(va, s))) return err;
+  }
+  return 0;
+}
+
 int pipe_init(DevCtx& c) {
   if (c.pipe_ready) return 0;
   if (c.pst[0].ensure(c.chunk) || c.pst[1].ensure(c.chunk)) return EDV_E_OOM;
@@ -684,6 +712,8 @@ int drain(DevCtx& c) {
   for (int q = 0; q < kQ; q++) HIPOK(hipStreamSynchronize(c.hs[q]), "stream sync");
   if (c.hcp) HIPOK(hipStreamSynchronize(c.hcp), "stream sync");
   if (c.hac) HIPOK(hipStreamSynchronize(c.hac), "stream sync");  // async batches stay pending until edv_wait_async
+  for (auto& s : c.as)
+    if (s.st) HIPOK(hipStreamSynchronize(s.st), "stream sync");
   if (c.pipe_ready) {
     HIPOK(hipStreamSynchronize(c.sp), "pipeline sync");
     HIPOK(hipStreamSynchronize(c.sm), "pipeline sync");
@@ -985,8 +1015,9 @@ int async_complete(DevCtx::AsyncSlot& s) {
 // Queue one host batch: H2D copies on hcp (from the caller's memory when it is
 // pinned, else through the slot's pinned staging, filled here while the
 // previous batch computes), then on hac the kernels and the D2H of the
-// verdicts.  A slot is reused kAsyncSlots submissions later, after its batch is
-// complete.  Caller holds c.mu.
+// verdicts; a batch of at most kSmallAsync requests does all of that on its
+// slot's own stream and scratch instead.  A slot is reused kAsyncSlots
+// submissions later, after its batch is complete.  Caller holds c.mu.
 int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
                  uint64_t n, uint8_t* accept, uint8_t* digests, int64_t* ticket) {
   const int64_t t = c.next_ticket;
@@ -997,6 +1028,13 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
   if (s.sigs.ensure(n * 64) || s.pks.ensure(n * 32) || s.msgs.ensure(mbytes + 64) || s.off.ensure((n + 1) * 8) ||
       s.acc.ensure(n) || (digests && s.dig.ensure(32 * n)))
     return EDV_E_OOM;
+  // small batch: everything on the slot's stream and scratch (see kSmallAsync)
+  const bool own = n <= kSmallAsync;
+  if (own) {
+    if (!s.st) HIPOK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking), "hipStreamCreate");
+    if (s.cb.ensure(kSmallAsync)) return EDV_E_OOM;
+  }
+  const hipStream_t cs = own ? s.st : c.hcp, ks = own ? s.st : c.hac;
   s.dig_pinned = digests && is_pinned(digests);
   if (digests && !s.dig_pinned && s.dig_host.ensure(32 * n)) return EDV_E_OOM;
   const bool pinned = is_pinned(sigs) && is_pinned(pks) && is_pinned(off) && (mbytes == 0 || is_pinned(msgs + mbase));
@@ -1018,26 +1056,29 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
   uint8_t* d_msgs = static_cast<uint8_t*>(s.msgs.p);
   uint64_t* d_off = static_cast<uint64_t*>(s.off.p);
   uint8_t* d_acc = static_cast<uint8_t*>(s.acc.p);
-  HIPOK(hipMemcpyAsync(d_sigs, src_s, n * 64, hipMemcpyHostToDevice, c.hcp), "h2d sigs");
-  HIPOK(hipMemcpyAsync(d_pks, src_p, n * 32, hipMemcpyHostToDevice, c.hcp), "h2d pks");
-  HIPOK(hipMemcpyAsync(d_off, src_o, (n + 1) * 8, hipMemcpyHostToDevice, c.hcp), "h2d off");
-  if (mbytes) HIPOK(hipMemcpyAsync(d_msgs, src_m, mbytes, hipMemcpyHostToDevice, c.hcp), "h2d msgs");
-  HIPOK(hipEventRecord(s.copied, c.hcp), "record");
-  HIPOK(hipStreamWaitEvent(c.hac, s.copied, 0), "wait copy");
-  if ((err = launch(c, d_sigs, d_pks, d_msgs, d_off, mbase, n, d_acc, c.hac,
-                    varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH)))
+  HIPOK(hipMemcpyAsync(d_sigs, src_s, n * 64, hipMemcpyHostToDevice, cs), "h2d sigs");
+  HIPOK(hipMemcpyAsync(d_pks, src_p, n * 32, hipMemcpyHostToDevice, cs), "h2d pks");
+  HIPOK(hipMemcpyAsync(d_off, src_o, (n + 1) * 8, hipMemcpyHostToDevice, cs), "h2d off");
+  if (mbytes) HIPOK(hipMemcpyAsync(d_msgs, src_m, mbytes, hipMemcpyHostToDevice, cs), "h2d msgs");
+  if (!own) {
+    HIPOK(hipEventRecord(s.copied, c.hcp), "record");
+    HIPOK(hipStreamWaitEvent(c.hac, s.copied, 0), "wait copy");
+  }
+  const uint32_t lflags = varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH;
+  if ((err = own ? launch_own(c, s.cb, kSmallAsync, d_sigs, d_pks, d_msgs, d_off, mbase, n, d_acc, ks, lflags)
+                 : launch(c, d_sigs, d_pks, d_msgs, d_off, mbase, n, d_acc, ks, lflags)))
     return err;
   uint8_t* h_acc = s.acc_pinned ? accept : static_cast<uint8_t*>(s.acc_host.p);
-  HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, c.hac), "d2h accept");
+  HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, ks), "d2h accept");
   if (digests) {
     // Request.getDigest of requests whose signing bytes ARE the message (the
     // caller decides which): SHA-256 of the same resident message bytes
     uint8_t* d_dig = static_cast<uint8_t*>(s.dig.p);
-    if ((err = launch_sha256(d_msgs, d_off, mbase, n, d_dig, c.hac))) return err;
+    if ((err = launch_sha256(d_msgs, d_off, mbase, n, d_dig, ks))) return err;
     uint8_t* h_dig = s.dig_pinned ? digests : static_cast<uint8_t*>(s.dig_host.p);
-    HIPOK(hipMemcpyAsync(h_dig, d_dig, 32 * n, hipMemcpyDeviceToHost, c.hac), "d2h digests");
+    HIPOK(hipMemcpyAsync(h_dig, d_dig, 32 * n, hipMemcpyDeviceToHost, ks), "d2h digests");
   }
-  HIPOK(hipEventRecord(s.done, c.hac), "record");
+  HIPOK(hipEventRecord(s.done, ks), "record");
   s.ticket = t;
   s.accept = accept;
   s.digests = digests;
@@ -1191,6 +1232,8 @@ int edv_verify_digest_batch_async(const uint8_t* sigs, const uint8_t* pks, const
     // buffers: let it finish before the caller gets the error back
     (void)hipStreamSynchronize(cl.c->hcp);
     (void)hipStreamSynchronize(cl.c->hac);
+    for (auto& s : cl.c->as)
+      if (s.st) (void)hipStreamSynchronize(s.st);
     (void)hipGetLastError();
   }
   return err;

@@ -61,6 +61,12 @@ static_assert(kBBits % kAWin == 0, "B digits must land on window boundaries");
 constexpr int kCombEntries = 129;               // signer comb rows: 0..128 x 256^i B
 constexpr int kBStride = 32;                    // words per B / comb entry (30 used; 128-byte aligned)
 
+EDV_HD int mx(int a, int b) { return a > b ? a : b; }
+// all ones iff x != 0, in plain VOP2 arithmetic: the or-value and the mask are
+// opaque, so LLVM can fold neither the shift nor a later AND with the mask
+// back into a compare and a VCC-mask v_cndmask_b32 (~23 cycles on gfx950)
+EDV_HD uint32_t nz_mask(uint32_t x) { return uint32_t(opaque_i32(opaque_i32(int32_t(x | (0u - x))) >> 31)); }
+
 // ------------------------------------------------------------- message words
 EDV_HD uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
   return uint32_t(((uint64_t(hi) << 32) | lo) >> (8 * sh));
@@ -93,11 +99,14 @@ EDV_HD void msg_words_tail(uint64_t* W, const uint8_t* m, uint64_t mlen, uint64_
   const uint32_t sh = uint32_t(a & 3);
   const uintptr_t base = a - sh;
   const uintptr_t last = (reinterpret_cast<uintptr_t>(m) + mlen) & ~uintptr_t(3);
+  const int32_t lim = int32_t(int64_t(last) - int64_t(base));  // < 0 for a block wholly past the end
   uint32_t d[2 * N + 1];
 #pragma unroll
   for (int t = 0; t < 2 * N + 1; t++) {
-    const uintptr_t ad = base + 4 * uintptr_t(t);
-    d[t] = *reinterpret_cast<const uint32_t*>(ad < last ? ad : last);
+    // min(base + 4t, last) as last - max(lim - 4t, 0): one v_max_i32 instead of
+    // a 64-bit compare and two VCC-mask selects
+    const int32_t back = lim - 4 * t;
+    d[t] = *reinterpret_cast<const uint32_t*>(last - uintptr_t(uint32_t(back > 0 ? back : 0)));
   }
   // byte masks without selects (a VCC-mask v_cndmask_b32 costs ~23 cycles on
   // gfx950): keep(k) = low k bytes set, as two shifts of at most 32 so k = 8 works
@@ -214,7 +223,31 @@ EDV_HD void recode16(uint32_t out[8], const uint32_t s[8]) { recode_signed<16, 1
 
 // Number of windows the packed radix-2^kAWin digits need: 1 + index of the
 // top nonzero digit (0 for a zero scalar).
+// bit length: one count-leading-zeros per word and an integer max, no selects
+// (a VCC-mask v_cndmask_b32 costs ~23 cycles on gfx950)
+EDV_HD int w8_bitlen(const uint32_t a[8]) {
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t x = a[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int lz = __builtin_clz(x);  // v_ffbh_u32; masked off for x == 0
+#else
+    const int lz = x ? __builtin_clz(x) : 32;
+#endif
+    n = mx(n, (32 * (i + 1) - lz) & int32_t(nz_mask(x)));
+  }
+  return n;
+}
+#ifndef EDV_NWIN_CLZ
+#define EDV_NWIN_CLZ 1
+#endif
 EDV_HD int digits5_windows(const uint32_t d[8]) {
+  if (EDV_NWIN_CLZ && kAWin == 4) {
+    // 4-bit fields never straddle a word: windows = ceil(bit length / 4) (the
+    // per-field scan below compiled to 64 v_cndmask_b32 per scalar)
+    return (w8_bitlen(d) + 3) >> 2;
+  }
   int n = 0;
 #pragma unroll
   for (int k = 0; k < kAWindows; k++) {
@@ -226,7 +259,6 @@ EDV_HD int digits5_windows(const uint32_t d[8]) {
 }
 
 // ------------------------------------------- 256-bit words (lattice reduction)
-EDV_HD int mx(int a, int b) { return a > b ? a : b; }
 EDV_HD bool w8_lt(const uint32_t a[8], const uint32_t b[8]) {
   bool lt = false, eq = true;
 #pragma unroll
@@ -254,12 +286,6 @@ EDV_HD void w8_sub(uint32_t a[8], const uint32_t b[8]) {
     br = s >> 32;
   }
 }
-EDV_HD int w8_bitlen(const uint32_t a[8]) {
-  int n = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) n = a[i] ? 32 * i + 32 - __builtin_clz(a[i]) : n;
-  return n;
-}
 EDV_HD double w8_to_f64(const uint32_t a[8]) {
   double d = 0.0;
 #pragma unroll
@@ -282,6 +308,23 @@ EDV_HD void w8_shr1(uint32_t a[8]) {
   a[7] >>= 1;
 }
 
+// a / b to about 2^-50 relative.  On the GPU: v_rcp_f64 and one Newton step
+// (4 instructions) in place of the IEEE-exact division sequence (div_scale x 2,
+// rcp, five fma, div_fmas, div_fixup); every caller corrects its quotient
+// afterwards, so exactness is not needed (see fdiv_floor and euclid_div).
+#ifndef EDV_RCP_DIV
+#define EDV_RCP_DIV 1
+#endif
+EDV_HD double approx_div(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (EDV_RCP_DIV) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+    return a * r;
+  }
+#endif
+  return a / b;
+}
 // One Euclidean division step of the lattice reduction: q = floor(r0 / r1)
 // (r0 >= r1 > 0), r0 <- r0 - q r1, t0 <- t0 - q t1 (cofactors signed, two's
 // complement mod 2^256).  q comes from a double-precision quotient of the two
@@ -289,7 +332,7 @@ EDV_HD void w8_shr1(uint32_t a[8]) {
 // q < 2^31 the estimate is q or q - 1 and one masked subtraction finishes it
 // (no branch); a larger quotient takes exact binary long division.
 EDV_HD void euclid_div(uint32_t r0[8], uint32_t t0[8], const uint32_t r1[8], const uint32_t t1[8]) {
-  const double qd = __builtin_floor(w8_to_f64(r0) / w8_to_f64(r1) * (1.0 - 0x1p-44));
+  const double qd = __builtin_floor(approx_div(w8_to_f64(r0), w8_to_f64(r1)) * (1.0 - 0x1p-44));
   uint32_t q = 0;
   if (qd < 2147483648.0) {
     q = uint32_t(qd);
@@ -346,20 +389,27 @@ EDV_HD bool w8_ge128(const uint32_t r[8]) { return (r[4] | r[5] | r[6] | r[7]) !
 // floor(r / 2^s) for r < 2^(s + 53), as an exact double
 EDV_HD double w8_window53(const uint32_t r[8], int s) {
   const int wi = s >> 5, b = s & 31;
+  // words wi, wi + 1, wi + 2 picked by arithmetic masks (per-lane index; the
+  // select form compiled to 24 VCC-mask v_cndmask_b32 at ~23 cycles each)
   uint32_t w0 = 0, w1 = 0, w2 = 0;
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    w0 = k == wi ? r[k] : w0;
-    w1 = k == wi + 1 ? r[k] : w1;
-    w2 = k == wi + 2 ? r[k] : w2;
+    const uint32_t d = uint32_t(k - wi);  // 0, 1, 2 for the three slots
+    const uint32_t m0 = ~nz_mask(d), m1 = ~nz_mask(d - 1u), m2 = ~nz_mask(d - 2u);
+    w0 |= r[k] & m0;
+    w1 |= r[k] & m1;
+    w2 |= r[k] & m2;
   }
   const uint64_t lo = (uint64_t(w1) << 32) | w0;
   const uint64_t v = b == 0 ? lo : ((lo >> b) | (uint64_t(w2) << (64 - b)));
   return double(v);
 }
-// floor(a / b) for exact non-negative integers a < 2^54, 0 < b < 2^54 in doubles
+// floor(a / b) for exact non-negative integers a < 2^54, 0 < b < 2^54 in doubles:
+// exact whenever the quotient is below 2^50 (the estimate is then within one
+// of it and the remainder test fixes that); larger quotients may be off, and
+// every caller rejects a quotient that large (Lehmer: cofactor above 2^30).
 EDV_HD double fdiv_floor(double a, double b) {
-  double q = __builtin_floor(a / b);
+  double q = __builtin_floor(approx_div(a, b));
   const double r = __builtin_fma(-q, b, a);
   q = r < 0 ? q - 1 : (r >= b ? q + 1 : q);
   return q;
@@ -393,7 +443,11 @@ EDV_HD bool lehmer_round(uint32_t r0[8], uint32_t r1[8], uint32_t t0[8], uint32_
     const double yc = y + C, yd = y + D;
     if (!(yc > 0 && yd > 0)) break;
     const double q = fdiv_floor(x + A, yc);
-    if (q != fdiv_floor(x + B, yd)) break;
+    // the other end of the interval gives the same quotient iff
+    // 0 <= (x + B) - q (y + D) < y + D: one fma (exact: an integer below 2^53
+    // whenever it is in range) instead of a second division
+    const double r2 = __builtin_fma(-q, yd, x + B);
+    if (!(r2 >= 0 && r2 < yd)) break;
     const double yn = x - q * y, Cn = A - q * C, Dn = B - q * D;
     // true next remainder > (yn - |Cn| - |Dn|) 2^s; keep the cofactors < 2^30
     if (yn - __builtin_fabs(Cn) - __builtin_fabs(Dn) < thr || __builtin_fabs(Cn) + __builtin_fabs(Dn) > 0x1p30) break;
@@ -490,24 +544,24 @@ EDV_HD void half_scalars(const uint32_t h[8], uint32_t a[8], uint32_t u[8], bool
   }
 }
 
-// (u * S) mod L for u < 2^256, S < 2^256 (8 words each)
+// (u * S) mod L for u < 2^256, S < 2^256 (8 words each).  Row by row: each
+// step u_i s_j + t_(i+j) + carry < 2^64 exactly, so it is one 32x32+64
+// multiply-add and one 64-bit add with no carry detection (the column form
+// needed a 64-bit compare and a select per product: 925 instructions, now ~200).
 EDV_HD void sc_mul(uint32_t out[8], const uint32_t u[8], const uint32_t s[8]) {
   uint32_t t[16];
-  uint64_t carry = 0;
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    uint64_t lo = carry, hi = 0;
+  for (int k = 0; k < 16; k++) t[k] = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const int j = k - i;
-      if (j < 0 || j > 7) continue;
-      const uint64_t p = uint64_t(u[i]) * s[j];
-      const uint64_t x = lo + p;
-      hi += (x < lo);
-      lo = x;
+  for (int i = 0; i < 8; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint64_t p = uint64_t(u[i]) * s[j] + t[i + j] + carry;
+      t[i + j] = uint32_t(p);
+      carry = p >> 32;
     }
-    t[k] = uint32_t(lo);
-    carry = (lo >> 32) | (hi << 32);
+    t[i + 8] = uint32_t(carry);
   }
   sc_reduce(out, t);
 }

@@ -53,6 +53,51 @@ def test_fe_mul_sq_against_python():
         assert val(h) % P == 2 * val(f) ** 2 % P and out_ok(h)
 
 
+def test_fe_sq_floor_chain():
+    """fe_sq_floor (the exponentiations' squaring runs): a signed reduced input
+    (what fe_mul returns) and then its own unsigned outputs, 40 squarings deep,
+    at the limb extremes of both forms: exact mod p, limbs in [0, 2^26) /
+    [0, 2^25) (h1 within 2^17), so the next squaring's premultiplied operands
+    stay inside int32."""
+    hc = hostcheck_lib.load()
+    r = random.Random(9)
+    h = (ctypes.c_int32 * 10)()
+    top = [(1 << 26) - 1 if i % 2 == 0 else (1 << 25) - 1 for i in range(10)]
+    starts = [[r.randrange(-2**25, 2**25) if i % 2 == 0 else r.randrange(-2**24, 2**24) for i in range(10)]
+              for _ in range(300)]
+    starts += [[(2**25 if i % 2 == 0 else 2**24) * s for i in range(10)] for s in (1, -1)]
+    starts += [top, [t if i != 1 else (1 << 25) + (1 << 17) for i, t in enumerate(top)]]
+    for f in starts:
+        x = val(f) % P
+        cur = f
+        for _ in range(40):
+            hc.hc_fe_sq_floor(arr(cur), h)
+            x = x * x % P
+            cur = list(h)
+            assert val(cur) % P == x
+            assert all(0 <= cur[i] < (1 << (26 if i % 2 == 0 else 25)) for i in range(10) if i != 1)
+            assert -(1 << 17) <= cur[1] < (1 << 25) + (1 << 17)
+
+
+def test_digits_windows():
+    """The window count from the packed 4-bit digits (count-leading-zeros form)
+    is 1 + the index of the top nonzero digit, 0 for no digits."""
+    hc = hostcheck_lib.load()
+    r = random.Random(11)
+    cases = [[0] * 8, [1] + [0] * 7, [0] * 7 + [0xF0000000], [0] * 7 + [1], [0x80000000] + [0] * 7]
+    for _ in range(3000):
+        w = [0] * 8
+        top = r.randrange(64)
+        for k in range(top + 1):
+            w[k // 8] |= r.randrange(16) << (4 * (k % 8))
+        w[top // 8] |= r.randrange(1, 16) << (4 * (top % 8))
+        cases.append(w)
+    for w in cases:
+        digits = [(w[k // 8] >> (4 * (k % 8))) & 15 for k in range(64)]
+        want = max([k + 1 for k in range(64) if digits[k]], default=0)
+        assert hc.hc_digits_windows((ctypes.c_uint32 * 8)(*w)) == want
+
+
 def test_fe_tobytes_canonical_and_frombytes():
     hc = hostcheck_lib.load()
     r = random.Random(6)

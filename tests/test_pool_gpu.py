@@ -47,3 +47,51 @@ def test_pool_c5_gpu_batched_equals_reference_flow(monkeypatch, overlap):
     assert set(gpu["ordered_keys"][0]) == set(cpu_digests(valid))
     assert gpu["verifies"] == ref["verifies"] == 4 * len(reqs) + 4 * 3 * len(valid)
     assert gpu["auth_calls"] < ref["auth_calls"] / 10    # one authenticate_batch per prod
+
+
+def _sodium():
+    import ctypes
+    for path in ("/opt/conda/lib/libsodium.so.23", "libsodium.so.23", "libsodium.so"):
+        try:
+            lib = ctypes.CDLL(path)
+        except OSError:
+            continue
+        lib.sodium_init()
+        return lib
+    return None
+
+
+def _sodium_open_batch(lib):
+    """crypto_sign_open(sig + msg, pk) on libsodium 1.0.18 itself (the library
+    the oracle is pinned to), same contract as edv.open_batch."""
+    import ctypes
+
+    def run(items, device_mask=0):
+        out = []
+        for s, m, p in items:
+            sm = bytes(s) + bytes(m)
+            buf = ctypes.create_string_buffer(len(sm))
+            mlen = ctypes.c_ulonglong(0)
+            out.append(lib.crypto_sign_open(buf, ctypes.byref(mlen), sm, ctypes.c_ulonglong(len(sm)), bytes(p)) == 0)
+        return out
+    return run
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_pool_c5_gpu_large_flood_equals_reference_flow(monkeypatch, overlap):
+    """The same check on a flood ten times larger (3,250 requests, 52,000
+    verifies per run), the reference flow's verifies on libsodium itself."""
+    lib = _sodium()
+    if lib is None:
+        pytest.skip("libsodium not present")
+    assert edv.device_count() >= 1
+    signers, reqs, valid = flood(n_valid=3000, n_bad_sig=200, n_unknown=50, seed=56)
+    with monkeypatch.context() as m:
+        m.setattr(edv, "open_batch", _sodium_open_batch(lib))
+        ref = _run(signers, reqs, valid, batched=False, digest_fn=cpu_digests)
+    gpu = _run(signers, reqs, valid, batched=True, digest_fn=digest.request_digests, overlap=overlap)
+    assert gpu["ordered_per_node"] == ref["ordered_per_node"] == [len(valid)] * 4
+    assert gpu["nacks_per_node"] == ref["nacks_per_node"] == [len(reqs) - len(valid)] * 4
+    assert gpu["bad_propagates"] == ref["bad_propagates"] == 0
+    assert gpu["ordered_keys"] == ref["ordered_keys"]
+    assert gpu["verifies"] == ref["verifies"] == 4 * len(reqs) + 4 * 3 * len(valid)
