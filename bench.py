@@ -590,13 +590,24 @@ def c4_leg(dev, steps, reps, n=65536):
     ops = float(np.sum(217600 + 5500 * ((lens + 81 + 127) // 128)))
     prep_ms, main_ms = edv.profile_device(b.d_sigs.ptr, b.d_pks.ptr, b.d_msgs.ptr, b.d_off.ptr, n, b.d_accept.ptr,
                                           dev, max(3, min(steps, 10)))
+    # the same batches through the two-stream pipeline (prep of step k+1 beside main of step k): at C4
+    # the prep kernel's SHA-512 tail runs one latency-bound wave per SIMD, so the overlap may pay here
+    for _ in range(3):
+        b.submit()
+    edv.pipeline_sync(dev)
+    tp = timed_steps(b.submit, lambda: edv.pipeline_sync(dev), steps, reps, rdv)
+    okp = bool(np.array_equal(b.accept(), exp))
     return {"workload": "C4: %d Ed25519 verifies per step, messages uniform in 200..4,096 B (mean %.0f B), "
                         "length-bucketed SHA-512, 5 %% invalid over %s" % (n, lens.mean(), ", ".join(workload.DAMAGE_KINDS)),
             "verifies_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps, "reps_s": ts,
             "verdicts_as_expected": ok, "invalid": int(n - exp.sum()),
             "prep_kernel_ms": prep_ms, "main_kernel_ms": main_ms,
             "roofline_frac": ops / ((prep_ms + main_ms) * 1e-3) / PEAK_INT32,
-            "w_ops_per_verify_mean": ops / n}
+            "w_ops_per_verify_mean": ops / n,
+            "pipelined": {"verifies_per_s": n * steps / statistics.median(tp), "reps_s": tp,
+                          "verdicts_as_expected": okp,
+                          "what": "edv_verify_batch_dev_pipelined back to back (prep of step k+1 on a second stream "
+                                  "beside main of step k)"}}
 
 
 def c5_leg(n=20000, n_cpu=2000):
