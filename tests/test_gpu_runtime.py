@@ -262,6 +262,51 @@ def test_host_async_path_from_threads():
     assert errors == []
 
 
+def test_host_async_small_batches_side_by_side():
+    """Small asynchronous batches (at most kSmallAsync = 8,192 requests: each
+    runs on its slot's own stream and scratch, side by side with the others)
+    from four threads at once, fixed and mixed lengths (length buckets), sizes
+    either side of the boundary (8,192 on a slot stream, 8,193 on the shared
+    one), then single-threaded with chunks smaller than the batches (the slot
+    path walks chunks on its own scratch).  Every verdict array equals the
+    checker."""
+    import threading
+    sizes = [1, 97, 400, 1000, 4096, 8191, 8192, 8193]
+    batches = [orc.corpus(0x5A11 + k, 0, n, mode=k % 2, invalid_permille=150) for k, n in enumerate(sizes)]
+    wants = [checker(*b) for b in batches]
+    errors = []
+
+    def worker(w):
+        try:
+            for rnd in range(3):
+                ks = [(w + rnd + j) % len(sizes) for j in range(3)]
+                accs = {k: np.full(sizes[k], 7, np.uint8) for k in ks}
+                ts = [(k, edv.verify_async(*batches[k], accs[k])) for k in ks]
+                for k, t in ts:
+                    edv.wait_async(t)
+                    assert np.array_equal(accs[k], wants[k]), (w, rnd, k)
+        except BaseException as ex:  # reported below, in the test's thread
+            errors.append(ex)
+
+    th = [threading.Thread(target=worker, args=(w,)) for w in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th)
+    assert errors == []
+    try:
+        edv.set_chunk(0, 1024)
+        accs = [np.full(n, 7, np.uint8) for n in sizes]
+        ts = [edv.verify_async(*b, a) for b, a in zip(batches, accs)]
+        for t in ts:
+            edv.wait_async(t)
+        for a, w in zip(accs, wants):
+            assert np.array_equal(a, w)
+    finally:
+        edv.set_chunk(0, 0)
+
+
 def test_host_path_chunk_seams_with_sub_batches():
     """Small chunks: the host path's sub-batches then span several chunk-sized
     scratch regions per stream (and one stream when the chunk is tiny)."""
