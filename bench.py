@@ -621,6 +621,9 @@ def c5_leg(n=20000, n_cpu=2000):
     out["summary"] = {"gpu_ordered_req_per_s": g["ordered_req_per_s_one_process"],
                       "gpu_auth_share_of_node_time": g["auth_share_of_node_time"],
                       "gpu_vs_no_verify_ceiling": out["overlap_vs_ceiling"],
+                      "gpu_vs_same_path_verify_skipped": out.get("overlap_vs_verify_skipped"),
+                      "verify_skipped_ordered_req_per_s": out.get("gpu_overlap_verify_skipped", {}).get(
+                          "ordered_req_per_s_one_process"),
                       "gpu_mode": "overlap: authenticate_batch_submit per prod, handed over at the next prod",
                       "cpu_ordered_req_per_s": out.get("cpu_reference", {}).get("ordered_req_per_s_one_process"),
                       "cpu_auth_share_of_node_time": out.get("cpu_reference", {}).get("auth_share_of_node_time")}

@@ -594,6 +594,9 @@ VerifyArgs make_args(const DevCtx& c, ChunkBufs& b, const uint8_t* d_sigs, const
 
 // [length buckets,] prep kernel of one chunk on stream s (ctr: this stream's histogram + cursors)
 int launch_prep(uint32_t* ctr, const VerifyArgs& va, const uint64_t* d_off, bool bucket, hipStream_t s) {
+#ifdef EDV_MEASURE_NO_VERIFY
+  return 0;  // measurement build: see launch_main
+#endif
   const unsigned blocks = unsigned((va.n + kBlock - 1) / kBlock);
   if (bucket) {
     HIPOK(hipMemsetAsync(ctr, 0, 2 * kBuckets * 4, s), "memset buckets");
@@ -606,6 +609,15 @@ int launch_prep(uint32_t* ctr, const VerifyArgs& va, const uint64_t* d_off, bool
   return 0;
 }
 int launch_main(const VerifyArgs& va, hipStream_t s) {
+#ifdef EDV_MEASURE_NO_VERIFY
+  // Measurement build only (variants/libedv_noverify.so, loaded by bench.py's
+  // C5 leg through EDV_LIB in a separate process, never the product library):
+  // every request of the chunk is reported valid without the verify kernels,
+  // so a pool run can tell what verification costs from what everything around
+  // it costs.  (A chunk's slots map onto accept[base, base + n), in any order.)
+  HIPOK(hipMemsetAsync(va.accept + va.base, 1, va.n, s), "memset accept");
+  return 0;
+#endif
   const unsigned blocks = unsigned((va.n + kBlock - 1) / kBlock);
   edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
   HIPOK(hipGetLastError(), "main launch");
@@ -1177,7 +1189,11 @@ int check_dev_align(const void* d_sigs, const void* d_pks, const void* d_off) {
 // ------------------------------------------------------------------ C-ABI
 extern "C" {
 
+#ifdef EDV_MEASURE_NO_VERIFY
+const char* edv_version(void) { return "edv 0.2.0 gfx950 MEASUREMENT-ONLY: verification skipped"; }
+#else
 const char* edv_version(void) { return "edv 0.2.0 gfx950"; }
+#endif
 const char* edv_last_error(void) { return g_err.c_str(); }
 
 int edv_device_count(void) {

@@ -102,6 +102,25 @@ def run(mode, clients, reqs):
     return st
 
 
+NOVERIFY_LIB = os.path.join(ROOT, "indy-plenum_amd", "variants", "libedv_noverify.so")
+
+
+def run_isolated(mode, n, lib):
+    """One pool run in a child process whose edv loads `lib` (EDV_LIB): the
+    measurement-only library that reports every request valid without running
+    the verify kernels.  Same flood, same host path, same digests on the GPU."""
+    import subprocess
+    env = dict(os.environ, EDV_LIB=lib)
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--mode", mode, "--n", str(n)],
+                       capture_output=True, text=True, env=env, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError("isolated pool run failed: %s" % r.stderr[-2000:])
+    st = json.loads(r.stdout.strip().splitlines()[-1])
+    if "MEASUREMENT-ONLY" not in st["library"]:
+        raise RuntimeError("the isolated run did not load the measurement library: %s" % st["library"])
+    return st
+
+
 def c5(n=20000, n_cpu=2000):
     """The C5 figures: GPU-batched (and overlapped) pool against the reference's
     one-message-at-a-time flow on libsodium, on the same harness."""
@@ -111,6 +130,12 @@ def c5(n=20000, n_cpu=2000):
            "gpu_batched": run("gpu_batched", clients, reqs),
            "gpu_batched_overlap": run("gpu_batched_overlap", clients, reqs),
            "no_verify_ceiling": run("no_verify_ceiling", clients, reqs)}
+    if os.path.exists(NOVERIFY_LIB):
+        # the GPU overlap path with the verify kernels skipped: if it orders no
+        # faster than the real one, the pool is not bound by signature verification
+        out["gpu_overlap_verify_skipped"] = run_isolated("gpu_batched_overlap", n, NOVERIFY_LIB)
+        out["overlap_vs_verify_skipped"] = (out["gpu_batched_overlap"]["ordered_req_per_s_one_process"]
+                                            / out["gpu_overlap_verify_skipped"]["ordered_req_per_s_one_process"])
     ceil = out["no_verify_ceiling"]["ordered_req_per_s_one_process"]
     out["overlap_vs_ceiling"] = out["gpu_batched_overlap"]["ordered_req_per_s_one_process"] / ceil
     out["batched_vs_ceiling"] = out["gpu_batched"]["ordered_req_per_s_one_process"] / ceil
@@ -125,4 +150,14 @@ def c5(n=20000, n_cpu=2000):
 
 
 if __name__ == "__main__":
-    print(json.dumps(c5(int(os.environ.get("N", 20000)), int(os.environ.get("N_CPU", 2000)))))
+    if "--mode" in sys.argv:
+        # one mode, one JSON line (run_isolated's child)
+        mode = sys.argv[sys.argv.index("--mode") + 1]
+        n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else 20000
+        clients, reqs = make_flood(n)
+        run(mode, clients, reqs[:500])
+        st = run(mode, clients, reqs)
+        st["library"] = edv.lib().edv_version().decode()
+        print(json.dumps(st))
+    else:
+        print(json.dumps(c5(int(os.environ.get("N", 20000)), int(os.environ.get("N_CPU", 2000)))))
