@@ -89,3 +89,28 @@ def test_async_entry_points_validate_and_fail_loudly():
             edv.verify_async(sigs, pks, msgs, off, acc)
         with pytest.raises(edv.EdvUnavailable):
             edv.wait_async(0)
+
+
+def test_product_library_is_never_the_measurement_build():
+    """The measurement-only build (variants/libedv_noverify.so: every request
+    reported valid, for bench.py's C5 comparison) is loaded only through an
+    explicit EDV_LIB in a child process; the product default is libedv.so,
+    which verifies."""
+    env_lib = os.environ.pop("EDV_LIB", None)
+    try:
+        code = ("import sys; sys.path.insert(0, %r); from indy_plenum_amd import edv; "
+                "print(edv.LIB_PATH); print(edv.version())" % ROOT)
+        r = subprocess.run(["python3", "-c", code], capture_output=True, text=True, timeout=60,
+                           env={k: v for k, v in os.environ.items() if k != "EDV_LIB"})
+        assert r.returncode == 0, r.stderr
+        path, ver = r.stdout.strip().splitlines()[-2:]
+        assert os.path.basename(path) == "libedv.so"
+        assert "MEASUREMENT-ONLY" not in ver
+    finally:
+        if env_lib is not None:
+            os.environ["EDV_LIB"] = env_lib
+    mlib = os.path.join(ROOT, "indy-plenum_amd", "variants", "libedv_noverify.so")
+    if os.path.exists(mlib):
+        m = ctypes.CDLL(mlib)
+        m.edv_version.restype = ctypes.c_char_p
+        assert b"MEASUREMENT-ONLY" in m.edv_version()
