@@ -9,7 +9,10 @@ tests/test_gpu_parity.py with fresh corpora of a different generator:
   C4  4,194,304 requests of 200..4,096 B, 5 % damaged over seven kinds
       (small-order R, non-canonical A, small-order A included)
 
-  python tools/parity_live_sodium.py [c3_total] [c4_total]
+  fuzz 2,097,152 requests of 256 B with random bit flips anywhere in sig, pk
+      or message, or a random R, S or A (host buffers through edv_verify_batch)
+
+  python tools/parity_live_sodium.py [c3_total] [c4_total] [fuzz_total]
 Prints one JSON line per workload and a summary; exit status 1 on any mismatch.
 """
 import json
@@ -52,14 +55,65 @@ def run(name, total, **kw):
     return out
 
 
+def fuzz(total, seed=0xF022):
+    """Random damage anywhere: from valid 256-B batches, per request one of
+    1-3 random bit flips over sig || pk || msg (45 %), a random 32-byte R, S
+    or A (5 % each), or left intact; verified through the C-ABI host path
+    (edv_verify_batch on host buffers)."""
+    from indy_plenum_amd import edv
+    t0 = time.time()
+    rng = np.random.default_rng(seed)
+    checked = mism = rejected = 0
+    first_bad = None
+    for start in range(0, total, SLICE):
+        n = min(SLICE, total - start)
+        b = workload.DeviceBatch(n, start=start, seed=seed, keep_host=True)
+        sigs, pks, msgs, off = b.host_copy()
+        del b
+        sigs = sigs.reshape(n, 64).copy()
+        pks = pks.reshape(n, 32).copy()
+        msgs = msgs.copy()
+        kind = rng.integers(0, 100, size=n)
+        flip = np.nonzero(kind < 45)[0]
+        for _ in range(3):
+            sel = flip[rng.random(flip.size) < 0.6]
+            pos = rng.integers(0, 64 + 32 + 256, size=sel.size)
+            bit = (np.uint8(1) << rng.integers(0, 8, size=sel.size).astype(np.uint8))
+            s_ = pos < 64
+            sigs[sel[s_], pos[s_]] ^= bit[s_]
+            p_ = (pos >= 64) & (pos < 96)
+            pks[sel[p_], pos[p_] - 64] ^= bit[p_]
+            m_ = pos >= 96
+            mo = off[sel[m_]].astype(np.int64) + (pos[m_] - 96)
+            msgs[mo] ^= bit[m_]
+        for lo_k, hi_k, arr, a, bb in ((45, 50, sigs, 0, 32), (50, 55, sigs, 32, 64), (55, 60, pks, 0, 32)):
+            sel = np.nonzero((kind >= lo_k) & (kind < hi_k))[0]
+            arr[sel, a:bb] = rng.integers(0, 256, size=(sel.size, bb - a), dtype=np.uint8)
+        got = edv.verify_arrays(sigs.reshape(-1), pks.reshape(-1), msgs, off)
+        want = orc.sodium_verify_batch(sigs.reshape(-1), pks.reshape(-1), msgs, off, 16)
+        bad = np.nonzero(got != want)[0]
+        if bad.size and first_bad is None:
+            first_bad = int(start + bad[0])
+        mism += int(bad.size)
+        checked += n
+        rejected += int(n - want.sum())
+    out = {"workload": "fuzz: random bit flips over sig/pk/msg and random R, S, A (256 B)", "requests": checked,
+           "libsodium_rejected": rejected, "mismatches": mism, "first_mismatch": first_bad,
+           "seconds": round(time.time() - t0, 1)}
+    print(json.dumps(out), flush=True)
+    return out
+
+
 def main():
     if orc.sodium_batch() is None:
         sys.exit("libsodium not present: nothing to compare against")
     c3 = int(sys.argv[1]) if len(sys.argv) > 1 else 16777216
     c4 = int(sys.argv[2]) if len(sys.argv) > 2 else 4194304
+    nf = int(sys.argv[3]) if len(sys.argv) > 3 else 2097152
     res = [run("C3 256 B, 5 % damaged (4 kinds)", c3, damage_every=20, damage_kinds=4),
            run("C4 200..4,096 B, 5 % damaged (7 kinds)", c4, seed=0xC4C4, var_range=(200, 4096), damage_every=20,
-               damage_kinds=7)]
+               damage_kinds=7),
+           fuzz(nf)]
     total = sum(r["requests"] for r in res)
     bad = sum(r["mismatches"] for r in res)
     print(json.dumps({"summary": "GPU vs libsodium 1.0.18, live", "requests": total, "mismatches": bad}))
