@@ -324,7 +324,7 @@ class Pool:
         for nd in self.nodes.values():
             pend, nd._pending = nd._pending, None
             if pend is not None:
-                nd._finish(*pend)
+                nd._finish(pend)
 
     def close(self):
         """Hand over whatever is still in flight (the pool stays usable)."""

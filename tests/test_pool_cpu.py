@@ -94,6 +94,27 @@ def test_pool_stall_raises(batched, overlap, monkeypatch):
         pool.close()
 
 
+def test_pool_run_ending_with_batches_in_flight(monkeypatch):
+    """overlap=True: a run that reaches its target while nodes still hold a
+    submitted prod hands those verdicts over in drain() (each message once),
+    and the pool then goes on to order the rest."""
+    monkeypatch.setattr(edv, "open_batch", lambda items, device_mask=0: H.oracle_open_batch(list(items)))
+    signers, reqs, valid = flood()
+    pool = Pool(factory(signers), n=4, batched=True, digest_fn=cpu_digests, overlap=True, client_quota=16,
+                max_batch=7)
+    pool.submit(reqs)
+    try:
+        pool.run(5)
+        assert all(nd._pending is None for nd in pool.nodes.values())
+        wall = pool.run(len(valid))
+    finally:
+        pool.close()
+    st = pool.stats(wall, len(valid))
+    assert st["ordered_per_node"] == [len(valid)] * 4
+    assert st["nacks_per_node"] == [len(reqs) - len(valid)] * 4
+    assert st["verifies"] == 4 * len(reqs) + 4 * 3 * len(valid)
+
+
 def test_pool_overlap_on_the_native_async_path(monkeypatch):
     """overlap=True through the real native asynchronous path (auth_core_submit /
     auth_core_finish, device digests) with the device calls answered by the
