@@ -620,6 +620,8 @@ def c5_leg(n=20000, n_cpu=2000):
     g = out["gpu_batched_overlap"]
     out["summary"] = {"gpu_ordered_req_per_s": g["ordered_req_per_s_one_process"],
                       "gpu_auth_share_of_node_time": g["auth_share_of_node_time"],
+                      "gpu_auth_share_excluding_gc": g.get("auth_share_excluding_gc"),
+                      "gpu_gc_share_of_node_time": g.get("gc_share_of_node_time"),
                       "gpu_vs_no_verify_ceiling": out["overlap_vs_ceiling"],
                       "gpu_vs_same_path_verify_skipped": out.get("overlap_vs_verify_skipped"),
                       "verify_skipped_ordered_req_per_s": out.get("gpu_overlap_verify_skipped", {}).get(

@@ -839,8 +839,13 @@ int pack_all(Batch& b, int threads) {
   uint8_t* base = b.ar->p;
   if (!g_pool) g_pool = new DecodePool();
   Py_BEGIN_ALLOW_THREADS
-  // about 100 requests per part: a part costs tens of microseconds, a hand-off a few
-  const int T = std::max(1, std::min({threads, 32, int(nf / 96)}));
+  // at least 1,024 requests per part: a Node prod's batch (a few hundred) decodes
+  // on the calling thread, 0.40 us per request for submission and decode on the
+  // MI355X box's host against 0.55-0.64 us with ~100-request parts on four
+  // threads (the hand-offs cost more than the decoding they share,
+  // profiles/r03/host_part_s22.log); only large batches spread out
+  constexpr int kPart = 1024;
+  const int T = std::max(1, std::min({threads, 32, int(nf / kPart)}));
   const std::function<void(int)> part = [&](int t) {
     const size_t lo = nf * size_t(t) / size_t(T), hi = nf * size_t(t + 1) / size_t(T);
     for (size_t i = lo; i < hi; i++)

@@ -33,6 +33,7 @@ the node's next prod, so the GPU round trip of one node's batch runs while the
 nodes do their Python work.  Each message is still handled exactly once with
 its own verdict, in arrival order; it is only handled one prod later.
 """
+import gc
 import hashlib
 import json
 import time
@@ -65,6 +66,45 @@ class _ReqState:
         self.forwarded = False
 
 
+class _GcClock:
+    """Seconds the cyclic GC ran, in total and while a node was inside its
+    authentication window (the GC runs when the process's allocation count
+    crosses a threshold, so a collection lands in whichever code allocates
+    next, and pays for every object the node made, not only the ones it made
+    there)."""
+
+    def __init__(self):
+        self.total_s = self.in_auth_s = 0.0
+        self.auth_depth = 0
+        self._t = None
+
+    def __call__(self, phase, _info):
+        if phase == "start":
+            self._t = time.perf_counter()
+        elif self._t is not None:
+            d = time.perf_counter() - self._t
+            self.total_s += d
+            if self.auth_depth:
+                self.in_auth_s += d
+            self._t = None
+
+
+class _AuthWindow:
+    """Adds the time spent inside it to node.auth_s."""
+    __slots__ = ("node", "t")
+
+    def __init__(self, node):
+        self.node = node
+
+    def __enter__(self):
+        self.node.gc_clock.auth_depth += 1
+        self.t = time.perf_counter()
+
+    def __exit__(self, *exc):
+        self.node.auth_s += time.perf_counter() - self.t
+        self.node.gc_clock.auth_depth -= 1
+
+
 class _TimedAuth:
     """ReqAuthenticator proxy adding the time spent inside it to node.auth_s."""
 
@@ -72,18 +112,12 @@ class _TimedAuth:
         self._auth, self._node = auth, node
 
     def authenticate(self, req):
-        t = time.perf_counter()
-        try:
+        with _AuthWindow(self._node):
             return self._auth.authenticate(req)
-        finally:
-            self._node.auth_s += time.perf_counter() - t
 
     def authenticate_batch(self, reqs):
-        t = time.perf_counter()
-        try:
+        with _AuthWindow(self._node):
             return self._auth.authenticate_batch(reqs)
-        finally:
-            self._node.auth_s += time.perf_counter() - t
 
     def authenticate_batch_submit(self, reqs, digests=False):
         # timed by the caller (PoolNode.prod), together with the hand-over
@@ -125,6 +159,7 @@ class PoolNode:
         self.auth_calls = 0
         self.busy_s = 0.0
         self.auth_s = 0.0             # time inside request authentication and request digests
+        self.gc_clock = _GcClock()    # replaced by the pool's shared clock
 
     # ------------------------------------------------------------------ I/O
     def send_all(self, msg):
@@ -152,15 +187,13 @@ class PoolNode:
             if props or clients:
                 self.verifies += len(props) + len(clients)
                 self.auth_calls += 1
-                ta = time.perf_counter()
-                self._pending = PendingProd(self.auth, clients, props, digests=True)
-                self.auth_s += time.perf_counter() - ta
+                with _AuthWindow(self):
+                    self._pending = PendingProd(self.auth, clients, props, digests=True)
             if pend is not None:
                 self._finish(pend)
         elif props or clients:
-            ta = time.perf_counter()
-            keys = self.digest_fn([m["request"] for m, _ in props] + [m for m, _ in clients])
-            self.auth_s += time.perf_counter() - ta
+            with _AuthWindow(self):
+                keys = self.digest_fn([m["request"] for m, _ in props] + [m for m, _ in clients])
             self._keys = iter(keys)
             self.verifies += len(props) + len(clients)
             self.auth_calls += 1 if self.batched else len(props) + len(clients)
@@ -175,10 +208,9 @@ class PoolNode:
 
     # overlap mode: the previous prod's verdicts and digests, handed over now
     def _finish(self, pend):
-        ta = time.perf_counter()
         # waits only for what did not overlap, and builds the verdict lists
-        keys = pend.digests(self.digest_fn)
-        self.auth_s += time.perf_counter() - ta
+        with _AuthWindow(self):
+            keys = pend.digests(self.digest_fn)
         self._keys = iter(keys)
         pend.finish(self._on_client, self._on_propagate)
 
@@ -295,6 +327,9 @@ class Pool:
         self.nodes = {nm: PoolNode(nm, [p for p in names if p != nm], auth_factory(nm), f, batched, digest_fn,
                                    overlap=overlap, **node_kw) for nm in names}
         self.nodes[names[0]].is_primary = True
+        self.gc_clock = _GcClock()
+        for nd in self.nodes.values():
+            nd.gc_clock = self.gc_clock
 
     def submit(self, reqs):
         """A client flood: every request sent to every node (as the client does)."""
@@ -306,17 +341,21 @@ class Pool:
     def run(self, expect, max_idle_rounds=50):
         """prod every node round-robin until `expect` requests are ordered on
         every node; returns the wall-clock seconds."""
-        t0 = time.perf_counter()
-        idle = 0
-        while min(nd.ordered for nd in self.nodes.values()) < expect:
-            work = sum(nd.prod(self) for nd in self.nodes.values())
-            idle = 0 if work else idle + 1
-            if idle > max_idle_rounds:
-                self.drain()
-                raise RuntimeError("pool stalled: ordered %s of %d" % ([nd.ordered for nd in self.nodes.values()],
-                                                                      expect))
-        self.drain()
-        return time.perf_counter() - t0
+        gc.callbacks.append(self.gc_clock)
+        try:
+            t0 = time.perf_counter()
+            idle = 0
+            while min(nd.ordered for nd in self.nodes.values()) < expect:
+                work = sum(nd.prod(self) for nd in self.nodes.values())
+                idle = 0 if work else idle + 1
+                if idle > max_idle_rounds:
+                    self.drain()
+                    raise RuntimeError("pool stalled: ordered %s of %d" % (
+                        [nd.ordered for nd in self.nodes.values()], expect))
+            self.drain()
+            return time.perf_counter() - t0
+        finally:
+            gc.callbacks.remove(self.gc_clock)
 
     def drain(self):
         """Overlap mode: handle every batch still in flight (its verdicts are
@@ -333,9 +372,16 @@ class Pool:
     def stats(self, wall_s, n_reqs):
         nodes = list(self.nodes.values())
         busy = max(nd.busy_s for nd in nodes)
+        auth, node = sum(nd.auth_s for nd in nodes), sum(nd.busy_s for nd in nodes)
+        g = self.gc_clock
         return {"ordered_per_node": [nd.ordered for nd in nodes], "nacks_per_node": [nd.nacks for nd in nodes],
                 "bad_propagates": sum(nd.bad_propagates for nd in nodes),
                 "verifies": sum(nd.verifies for nd in nodes), "auth_calls": sum(nd.auth_calls for nd in nodes),
                 "wall_s": wall_s, "ordered_req_per_s_one_process": n_reqs / wall_s,
                 "max_node_busy_s": busy, "ordered_req_per_s_parallel_nodes": n_reqs / busy,
-                "auth_share_of_node_time": sum(nd.auth_s for nd in nodes) / sum(nd.busy_s for nd in nodes)}
+                "auth_share_of_node_time": auth / node,
+                # the cyclic GC's time, in total and the part that landed inside
+                # authentication windows; the share with every collection taken
+                # out of both node time and authentication time
+                "gc_share_of_node_time": g.total_s / node, "gc_in_auth_s": g.in_auth_s,
+                "auth_share_excluding_gc": (auth - g.in_auth_s) / max(node - g.total_s, 1e-12)}
