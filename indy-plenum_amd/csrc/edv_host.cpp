@@ -867,14 +867,21 @@ int pack_all(Batch& b, int threads) {
   return 0;
 }
 
-// phase D: (out, slow, rejected[, digests]).  The cyclic GC is paused while the
-// per-request lists are made: tens of thousands of new containers would
-// otherwise trigger repeated collections that walk every live object of the
-// node (30 ms per 64k batch, measured); the young objects are collected once, after.
+// phase D: (out, slow, rejected[, digests]).  For a large batch the cyclic GC
+// is paused while the per-request lists are made: tens of thousands of new
+// containers would otherwise trigger repeated collections that walk every live
+// object of the node (30 ms per 64k batch, measured); the young objects are
+// collected once, after.  A Node prod's batch (a few hundred requests) leaves
+// the GC alone: pausing it would only move a collection that the node's own
+// allocations made due to the first allocation after the pause, i.e. into the
+// caller's authentication step (req_authenticator.GC_PAUSE_MIN, same bound).
+constexpr Py_ssize_t kGcPauseMin = 4096;
+inline int gc_pause_for(Py_ssize_t n) { return n >= kGcPauseMin ? PyGC_Disable() : 0; }
+
 PyObject* build_output(Batch& b, bool with_digests) {
   const size_t nf = b.items.size();
   const uint8_t* acc = nf ? b.ar->p + b.o_acc : nullptr;
-  const int gc_was = PyGC_Disable();
+  const int gc_was = gc_pause_for(b.n);
   PyObject *out = PyList_New(b.n), *slow = PyList_New(0), *rejected = PyList_New(0), *digs = nullptr, *res = nullptr;
   if (with_digests) digs = PyList_New(b.n);
   if (!out || !slow || !rejected || (with_digests && !digs)) goto fail;
@@ -1194,7 +1201,7 @@ PyObject* py_req_auth_finish(PyObject*, PyObject* args) {
   }
   const size_t nf = b->items.size();
   const uint8_t* acc = nf ? b->ar->p + b->o_acc : nullptr;
-  const int gc_was = PyGC_Disable();
+  const int gc_was = gc_pause_for(b->n_all);
   PyObject *out = PyList_New(b->n_all), *slow = PyList_New(0), *general = PyList_New(0), *digs = nullptr;
   PyObject* res = nullptr;
   if (b->want_dig) digs = PyList_New(b->n_all);
