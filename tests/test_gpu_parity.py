@@ -82,6 +82,60 @@ def test_variable_length_c4_vs_libsodium():
     assert np.array_equal(got, checker(sigs, pks, msgs, off))
 
 
+def _signed_lengths(lens, seed):
+    """Requests of the given message lengths, signed by the oracle (libsodium's
+    algorithm), a fifth of them damaged: a message bit (often the last byte of a
+    long message), an R bit or an S bit."""
+    import random
+    r = random.Random(seed)
+    sigs, pks, msgs = [], [], []
+    for i, n in enumerate(lens):
+        pk, sk = orc.keypair(bytes([i & 255, i >> 8, seed & 255]) * 10 + b"LM")
+        m = bytearray(r.getrandbits(8) for _ in range(min(n, 4096))) * (n // 4096 + 1)
+        m = m[:n]
+        sig = bytearray(orc.sign(bytes(m), sk))
+        k = r.randrange(15)
+        if n == 0 and k == 1:
+            k = 2
+        if k == 1:
+            m[n - 1 if r.random() < 0.5 else r.randrange(n)] ^= 1 << r.randrange(8)
+        elif k == 2:
+            sig[r.randrange(32)] ^= 1 << r.randrange(8)
+        elif k == 3:
+            sig[32 + r.randrange(31)] ^= 1 << r.randrange(8)
+        sigs.append(bytes(sig))
+        pks.append(pk)
+        msgs.append(bytes(m))
+    off = np.zeros(len(lens) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    return (np.frombuffer(b"".join(sigs), np.uint8), np.frombuffer(b"".join(pks), np.uint8),
+            np.frombuffer(b"".join(msgs) + b"\0" * 16, np.uint8), off)
+
+
+def test_long_and_skewed_message_lengths():
+    """Message lengths far outside C2/C4 (up to 1 MiB, as the reference's verify
+    accepts any length) and around SHA-512 block boundaries, with a few very long
+    messages among many short ones (one length bucket holding them all, another
+    holding the rest), at the batch's start, middle and end, and across chunk
+    seams; verdicts equal libsodium's (the oracle where it is absent)."""
+    import random
+    r = random.Random(0x10C)
+    edges = [0, 1, 46, 47, 48, 63, 64, 111, 112, 113, 127, 128, 129, 175, 176, 239, 240, 241, 255, 256, 4096]
+    long_ = [1 << 14, (1 << 16) + 3, 1 << 18, 1 << 20]
+    lens = [1 << 20] + [r.choice(edges) for _ in range(700)] + long_ + [r.randrange(2000) for _ in range(700)] \
+        + [(1 << 20) - 1]
+    sigs, pks, msgs, off = _signed_lengths(lens, 0x5A)
+    want = checker(sigs, pks, msgs, off)
+    assert 0.65 < want.mean() < 0.95
+    assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off), want)
+    try:
+        for chunk in (256, 1024):
+            edv.set_chunk(0, chunk)
+            assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off), want), chunk
+    finally:
+        edv.set_chunk(0, 0)
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_chunk_seams(mode):
     """Batches spanning several prep/main chunk pairs (chunk forced small); mode 1
