@@ -380,6 +380,35 @@ def _bench(args, env=None, launcher=None, timeout=420):
 _QUICK = ["--steps", "2", "--reps", "2", "--warmup", "1", "--warmup-seconds", "0", "--no-cpu-baseline"]
 
 
+def test_bench_default_line_contract():
+    """The N = 1 line the driver reads (C2, legs off): the contract's keys, the
+    roofline object (bound, achieved = W ops / kernel time, peak, unit, frac =
+    achieved / peak, traffic from the PMC summary while the kernel sources match
+    it, else null) and the CPU baseline object with its sample and thread count."""
+    import bench
+    line = _bench(["--steps", "3", "--reps", "2", "--warmup", "1", "--warmup-seconds", "0", "--no-e2e",
+                   "--no-extra"])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line, k
+    assert line["n_gpus"] == 1 and line["steps"] == 3 and line["higher_is_better"] is True
+    assert line["unit"] == "verifies/s" and line["dtype"] == "int32" and line["scaling"] == "weak"
+    assert line["config"]["workload"].startswith("C2") and line["config"]["batch_per_gpu"] == 65536
+    assert line["verdicts_as_expected"] is True
+    rf = line["roofline"]
+    assert rf["unit"] == "TOP/s" and rf["peak"] > 0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
+    ops = rf["ops_per_launch"] / (rf["kernel_ms"] * 1e-3) / 1e12
+    assert abs(ops - rf["achieved"]) / rf["achieved"] < 1e-6
+    assert abs(rf["kernel_ms"] - rf["prep_kernel_ms"] - rf["main_kernel_ms"]) < 1e-6
+    assert rf["kernel_ms"] <= line["ms_per_step"] * 1.05
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                           "pmc_latest.json")) as f:
+        pmc_matches = json.load(f).get("kernel_source_sha256") == bench.kernel_source_hash()
+    assert (rf["traffic"] is not None) == pmc_matches
+    cb = line["cpu_baseline"]
+    assert cb["kind"] in ("reference", "port") and cb["value"] > 0 and cb["cores"] >= 1 and cb["sample"]
+
+
 def test_bench_c3_mode_bounded():
     """bench.py --total (C3 split by request index, 5 % damaged at known
     positions over four kinds, accept bytes checked) on a bounded total."""
