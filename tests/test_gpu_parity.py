@@ -150,6 +150,21 @@ def test_chunk_seams(mode):
         edv.set_chunk(0, 0)  # back to the default
 
 
+def test_fuzzed_damage_vs_libsodium():
+    """Random damage anywhere (tools/parity_live_sodium.py's fuzz corpus, one
+    2^16 slice): 1-3 random bit flips over sig || pk || msg, or a random R, S
+    or A, on valid C2 requests made by the GPU signer; verdicts equal
+    libsodium's (the oracle where it is absent)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import parity_live_sodium as pl
+    if orc.sodium_batch() is None:
+        pytest.skip("libsodium batch harness absent")
+    out = pl.fuzz(65536, seed=0xF1)
+    assert out["requests"] == 65536 and out["mismatches"] == 0, out
+    assert 0.4 < out["libsodium_rejected"] / 65536 < 0.8
+
+
 def test_full_size_c2_properties():
     """BASELINE configs[1] size (65,536 x 256 B, distinct signers): all valid
     accept; every kind of single-bit/malleation damage rejects exactly where applied."""
