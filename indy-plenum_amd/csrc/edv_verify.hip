@@ -785,6 +785,23 @@ void par_copy(const std::vector<Seg>& segs) {
 }
 
 uint64_t sha512_blocks(const uint64_t* off, uint64_t i) { return (64 + (off[i + 1] - off[i]) + 17 + 127) / 128; }
+// One branch-free pass over the offsets of requests [lo, hi): are they
+// non-decreasing, and do all messages have request lo's SHA-512 block count?
+// (It vectorises: at C2 the two early-exit loops it replaces took ~0.1 ms of a
+// synchronous call's host time before the first copy.)
+struct OffScan {
+  bool ok, uniform;
+};
+OffScan scan_offsets(const uint64_t* off, uint64_t lo, uint64_t hi) {
+  const uint64_t nb0 = sha512_blocks(off, lo);
+  uint64_t bad = 0, diff = 0;
+  for (uint64_t i = lo; i < hi; i++) {
+    const uint64_t a = off[i], b = off[i + 1];
+    bad |= uint64_t(b < a);
+    diff |= ((64 + (b - a) + 17 + 127) >> 7) ^ nb0;  // garbage when b < a: then bad is set
+  }
+  return {bad == 0, diff == 0};
+}
 
 // Parts for the split-prep host path, 0 = not used.  A shard of one chunk
 // whose messages all have the same SHA-512 block count (no length buckets) is
@@ -901,11 +918,7 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
   const bool acc_pinned = is_pinned(accept + lo);
   if (!acc_pinned && c.acc_host.ensure(n)) return EDV_E_OOM;
   // bucket by SHA block count only when the shard's messages differ in block count
-  bool varied = false;
-  {
-    const uint64_t nb0 = sha512_blocks(off, lo);
-    for (uint64_t i = lo + 1; i < hi && !varied; i++) varied = sha512_blocks(off, i) != nb0;
-  }
+  const bool varied = !scan_offsets(off, lo, hi).uniform;
   const uint32_t flags = varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH;
   uint8_t* d_sigs = static_cast<uint8_t*>(c.sigs.p);
   uint8_t* d_pks = static_cast<uint8_t*>(c.pks.p);
@@ -1052,8 +1065,7 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
   const bool pinned = is_pinned(sigs) && is_pinned(pks) && is_pinned(off) && (mbytes == 0 || is_pinned(msgs + mbase));
   s.acc_pinned = is_pinned(accept);
   if (!s.acc_pinned && s.acc_host.ensure(n)) return EDV_E_OOM;
-  bool varied = false;
-  for (uint64_t i = 1; i < n && !varied; i++) varied = sha512_blocks(off, i) != sha512_blocks(off, 0);
+  const bool varied = !scan_offsets(off, 0, n).uniform;
   const uint8_t *src_s = sigs, *src_p = pks, *src_m = msgs + mbase;
   const uint8_t* src_o = reinterpret_cast<const uint8_t*>(off);
   if (!pinned) {
@@ -1111,12 +1123,8 @@ constexpr uint64_t kVerifyBlocks = 40;
 void shard_bounds(const uint64_t* off, uint64_t n, uint32_t g, uint64_t* b) {
   b[0] = 0;
   b[g] = n;
-  bool uniform = true;
-  if (n > 0) {
-    const uint64_t nb0 = sha512_blocks(off, 0);
-    for (uint64_t i = 1; i < n && uniform; i++) uniform = sha512_blocks(off, i) == nb0;
-  }
-  if (uniform) {
+  if (g == 1) return;
+  if (n == 0 || scan_offsets(off, 0, n).uniform) {
     for (uint32_t k = 1; k < g; k++) b[k] = uint64_t((unsigned __int128)n * k / g);
     return;
   }
@@ -1171,8 +1179,7 @@ int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard 
 }
 
 int check_offsets(const uint64_t* msg_off, uint64_t n) {
-  for (uint64_t i = 0; i < n; i++)
-    if (msg_off[i + 1] < msg_off[i]) return set_err(EDV_E_ARG, "msg_off not non-decreasing");
+  if (!scan_offsets(msg_off, 0, n).ok) return set_err(EDV_E_ARG, "msg_off not non-decreasing");
   return 0;
 }
 
