@@ -722,27 +722,47 @@ struct Batch {
 // (client_authn.py:174, :222-223).  The two are the same bytes exactly when the
 // request's other keys are identifier, reqId, operation and, unless it is None,
 // protocolVersion.  -1 = error.
+// Which of the request keys digest_is_signing_bytes cares about k is: 1
+// signature / signatures / fees, 2 identifier / operation / reqId, 3
+// protocolVersion, 0 any other.  Keys of a JSON-decoded request are equal to,
+// not the same objects as, the interned names, so after the identity test one
+// length switch and at most two memcmp (ASCII compact strings), not a chain of
+// PyUnicode_CompareWithASCIIString calls per key.
+int signing_key_kind(PyObject* k) {
+  if (k == g_k_signature || k == g_k_signatures || k == g_k_fees) return 1;
+  if (k == g_k_identifier || k == g_k_operation || k == g_k_reqid) return 2;
+  if (k == g_k_protocol) return 3;
+  if (PyUnicode_READY(k) < 0) {
+    PyErr_Clear();
+    return 0;
+  }
+  if (!PyUnicode_IS_COMPACT_ASCII(k)) return 0;  // none of the names
+  const char* p = static_cast<const char*>(PyUnicode_DATA(k));
+  auto eq = [p](const char* t, size_t n) { return memcmp(p, t, n) == 0; };
+  switch (PyUnicode_GET_LENGTH(k)) {
+    case 4: return eq("fees", 4) ? 1 : 0;
+    case 5: return eq("reqId", 5) ? 2 : 0;
+    case 9: return eq("signature", 9) ? 1 : (eq("operation", 9) ? 2 : 0);
+    case 10: return eq("signatures", 10) ? 1 : (eq("identifier", 10) ? 2 : 0);
+    case 15: return eq("protocolVersion", 15) ? 3 : 0;
+    default: return 0;
+  }
+}
+
 int digest_is_signing_bytes(PyObject* req) {
   Py_ssize_t pos = 0;
   PyObject *k, *v;
   int have = 0;
-  auto is = [](PyObject* key, PyObject* interned, const char* text) {
-    return key == interned || PyUnicode_CompareWithASCIIString(key, text) == 0;
-  };
   while (PyDict_Next(req, &pos, &k, &v)) {
-    // keys of a JSON-decoded request are equal to, not the same objects as, the
-    // interned names: compare by value when identity fails
     if (!PyUnicode_CheckExact(k)) return 0;
-    if (is(k, g_k_signature, "signature") || is(k, g_k_signatures, "signatures") || is(k, g_k_fees, "fees")) continue;
-    if (is(k, g_k_identifier, "identifier") || is(k, g_k_operation, "operation") || is(k, g_k_reqid, "reqId")) {
-      have++;
-      continue;
+    switch (signing_key_kind(k)) {
+      case 1: continue;
+      case 2: have++; continue;
+      case 3:
+        if (v == Py_None) return 0;
+        continue;
+      default: return 0;  // any other key is in the signing bytes but not in signingState
     }
-    if (is(k, g_k_protocol, "protocolVersion")) {
-      if (v == Py_None) return 0;
-      continue;
-    }
-    return 0;  // any other key is in the signing bytes but not in signingState
   }
   return have == 3 ? 1 : 0;
 }
