@@ -44,6 +44,7 @@ harness oracle/sodium_batch.c, i.e. the reference's own CPU path).
 """
 import argparse
 import json
+import math
 import os
 import platform
 import socket
@@ -161,14 +162,25 @@ def cpu_info():
         pass
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
     quota = None
-    try:
+    try:  # cgroup v2
         with open("/sys/fs/cgroup/cpu.max") as f:
             q, per = f.read().split()
             quota = None if q == "max" else float(q) / float(per)
     except (OSError, ValueError):
-        pass
-    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota, "model": model,
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+        try:  # cgroup v1
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = float(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = float(f.read())
+            quota = q / per if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    ncpu = aff or os.cpu_count() or 1
+    # the CPUs this process can actually keep busy: its affinity, capped by the
+    # cgroup's CPU-time quota (on the GPU box: 256 CPUs visible, 16 CPUs of time)
+    effective = max(1, min(ncpu, int(math.ceil(quota)))) if quota else ncpu
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota, "effective_cpus": effective,
+            "model": model, "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 # ------------------------------------------------------------------ ranks
@@ -309,11 +321,33 @@ def rank_env():
     return world, rank, local, token
 
 
+def narrow_to_own_gpu(local, world):
+    """Before anything loads the HIP runtime: make this rank's GPU the only one
+    it sees (HIP_VISIBLE_DEVICES = the LOCAL_RANK-th visible device), so each
+    rank initialises one GPU, not all of them.  Returns the device index the
+    rank then drives (0), or `local` unchanged when the ranks share logical
+    devices of one GPU (EDV_VIRTUAL_DEVICES rehearsal) or there is one rank."""
+    if world == 1 or os.environ.get("EDV_VIRTUAL_DEVICES"):
+        return local, None
+    vis = os.environ.get("HIP_VISIBLE_DEVICES")
+    ids = [x.strip() for x in vis.split(",") if x.strip()] if vis is not None else None
+    if ids == []:
+        return local, None   # nothing visible: the device check below says so
+    if ids is not None and local >= len(ids):
+        sys.exit("bench.py: rank %d needs visible device %d, but HIP_VISIBLE_DEVICES=%s" % (local, local, vis))
+    own = ids[local] if ids is not None else str(local)
+    os.environ["HIP_VISIBLE_DEVICES"] = own
+    return 0, own
+
+
 # --------------------------------------------------------------- CPU baseline
 def cpu_baseline(batch, budget_s):
-    """libsodium 1.0.18 verify_detached over the same batch on the host cores:
-    all the cores this process may run on, the box's 16-CPU share, and one
-    thread; plus the reference's single-threaded Python chain on C1 (10k)."""
+    """libsodium 1.0.18 verify_detached over the same batch on the host cores
+    this process can actually use: effective_cpus = its CPU affinity capped by
+    the cgroup CPU quota (more threads than that only time-slice the same CPU
+    share).  Also the one-thread rate, and from it a labelled projection to
+    every core of the socket, which cannot be measured under the quota; plus
+    the reference's single-threaded Python chain on C1 (10k)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as orc  # the baseline leg is the only oracle/ user here
     sb = orc.sodium_batch()
@@ -321,35 +355,36 @@ def cpu_baseline(batch, budget_s):
         return None
     sigs, pks, msgs, off = batch.host_copy()
     info = cpu_info()
-    ncpu = info["affinity_cpus"] or info["nproc"] or 1
+    eff = info["effective_cpus"]
     n = batch.n
-    acc = orc.sodium_verify_batch(sigs, pks, msgs, off, min(16, ncpu))  # warm + sanity
+    acc = orc.sodium_verify_batch(sigs, pks, msgs, off, eff)  # warm + sanity
     assert np.array_equal(acc, batch.expected())
 
-    def rate(threads, seconds):
+    def rate(threads, seconds, k=n):
         done, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < seconds:
-            orc.sodium_verify_batch(sigs, pks, msgs, off, threads)
-            done += n
-        dt = time.perf_counter() - t0
-        return done / dt, done // n, dt
+        while True:
+            orc.sodium_verify_batch(sigs[:64 * k], pks[:32 * k], msgs, off[:k + 1], threads)
+            done += k
+            dt = time.perf_counter() - t0
+            if dt >= seconds:
+                return done / dt, done // k, dt
 
-    all_threads = min(512, ncpu)
-    v_all, p_all, t_all = rate(all_threads, budget_s)
-    share = min(16, ncpu)
-    v_share, p_share, t_share = rate(share, budget_s / 2) if share != all_threads else (v_all, p_all, t_all)
-    k = min(n, 16384)
-    t1 = time.perf_counter()
-    orc.sodium_verify_batch(sigs[:64 * k], pks[:32 * k], msgs, off[:k + 1], 1)
-    one = k / (time.perf_counter() - t1)
-    out = {"value": v_all, "unit": "verifies/s", "cores": all_threads, "kind": "reference",
+    v_eff, p_eff, t_eff = rate(eff, budget_s)
+    k1 = min(n, 8192)
+    v_one, p_one, t_one = rate(1, max(2.0, budget_s / 4), k1)
+    nproc = info["nproc"] or eff
+    out = {"value": v_eff, "unit": "verifies/s", "cores": eff, "kind": "reference",
            "sample": "%d passes over the %d-request batch (%d B msgs): libsodium %s crypto_sign_ed25519_verify_detached "
-                     "(oracle/sodium_batch.c), %d threads = every CPU this process may use, %.1f s"
-                     % (p_all, n, int(off[1] - off[0]), sb.sb_version().decode(), all_threads, t_all),
-           "all_cores_verifies_per_s": v_all, "all_cores_threads": all_threads,
-           "share_verifies_per_s": v_share, "share_threads": share,
-           "share_sample": "%d passes, %.1f s (16 threads: the box's CPU share per GPU)" % (p_share, t_share),
-           "one_thread_verifies_per_s": one, "host": info}
+                     "(oracle/sodium_batch.c) on %d threads = the CPUs this process can use (affinity %s, cgroup "
+                     "quota %s CPUs), %.1f s"
+                     % (p_eff, n, int(off[1] - off[0]), sb.sb_version().decode(), eff, info["affinity_cpus"],
+                        info["cgroup_cpu_quota"], t_eff),
+           "per_core_verifies_per_s": v_one,
+           "per_core_sample": "1 thread, %d passes over the first %d requests, %.1f s" % (p_one, k1, t_one),
+           "full_socket_projection_verifies_per_s": v_one * nproc,
+           "full_socket_projection_note": "projection, not measurable under the quota: per-core rate x nproc (%d)"
+                                          % nproc,
+           "host": info}
     try:
         out["c1_python_chain"] = c1_chain()
     except Exception as ex:  # the chain needs libsodium via ctypes; report why it is missing
@@ -550,19 +585,24 @@ def node_path_leg(n=65536, reps=3):
                                      "one GPU SHA-256 batch"}}
 
 
-def timed_steps(step, drain, steps, reps, rdv):
+def timed_steps(step, drain, steps, reps, rdv, only_rank=None, own=None):
     """R repetitions of `steps` steps, each between barrier + sync; max over
-    ranks per repetition -> list of seconds."""
+    ranks per repetition -> list of seconds.  only_rank: that rank alone runs
+    the steps (the others wait at the barriers).  own: gets this rank's time of
+    each repetition."""
     out = []
     for _ in range(max(1, reps)):
         drain()
         rdv.barrier()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
-        drain()
+        if only_rank is None or rdv.rank == only_rank:
+            for _ in range(steps):
+                step()
+            drain()
         t1 = time.perf_counter()
         rdv.barrier()
+        if own is not None:
+            own.append(t1 - t0)
         out.append(rdv.max(t1 - t0))
     return out
 
@@ -663,13 +703,13 @@ def main():
     world, rank, local, token = rank_env()
     if world != args.gpus:
         sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    dev, own_gpu = narrow_to_own_gpu(local, world)
 
     from indy_plenum_amd import edv, shard, workload
     ndev = edv.device_count()
-    if local >= ndev:
+    if dev >= ndev:
         sys.exit("bench.py: rank %d needs device %d, but %d gfx950 device(s) are visible (--gpus %d)"
-                 % (rank, local, ndev, args.gpus))
-    dev = local
+                 % (rank, dev, ndev, args.gpus))
     rdv = Rendezvous(rank, world, token)
 
     c3 = args.total > 0 or (world > 1 and not args.weak)
@@ -707,10 +747,17 @@ def main():
     warm_steps = done
     assert np.array_equal(batch.accept(), batch.expected()), "warm-up verdicts differ from the expected ones"
 
-    reps = timed_steps(step, drain, args.steps, args.reps, rdv)
+    alone = None
+    if world > 1:
+        # the same workload on one GPU: rank 0 times its own shard while the other
+        # ranks wait at the barrier (one repetition of K steps), before the joint reps
+        alone = timed_steps(step, drain, args.steps, 1, rdv, only_rank=0)[0]
+    mine_s = []
+    reps = timed_steps(step, drain, args.steps, args.reps, rdv, own=mine_s)
     elapsed = statistics.median(reps)
     ms_step = 1e3 * elapsed / args.steps
     value = total * args.steps / elapsed
+    per_rank_s = [struct.unpack("<d", g)[0] for g in rdv.gather(struct.pack("<d", statistics.median(mine_s)))]
 
     # per-kernel durations (HIP events on the kernels' own stream) on the first
     # chunk-sized slice of this rank's batch
@@ -752,6 +799,19 @@ def main():
                               "kernel time); peak = 256 CU x 64 lanes x 2.4 GHz (4-cycle VOP3 issue)"}
     if pmc:
         roofline.update(pmc)
+    if world > 1:
+        one_gpu = n * args.steps / alone   # rank 0's shard, timed alone
+        out_multi = {"per_rank_s": per_rank_s, "slowest_rank": int(np.argmax(per_rank_s)),
+                     "slowest_rank_s": max(per_rank_s), "per_rank_what": "each rank's median repetition "
+                     "(%d steps), its own clock between the barriers" % args.steps,
+                     "one_gpu_same_workload_verifies_per_s": one_gpu,
+                     "one_gpu_same_workload_what": "rank 0's shard (%d requests per step) timed alone, %d steps, the "
+                                                   "other ranks idle at a barrier, before the joint repetitions"
+                                                   % (n, args.steps),
+                     "scaling_efficiency": value / (world * one_gpu),
+                     "gpu_isolation": ("HIP_VISIBLE_DEVICES=<the LOCAL_RANK-th device> per rank" if own_gpu is not None
+                                       else "EDV_VIRTUAL_DEVICES=%s: logical devices sharing the visible GPU(s) "
+                                            "(rehearsal)" % os.environ.get("EDV_VIRTUAL_DEVICES"))}
     if c3:
         config = {"workload": "C3: %d Ed25519 verifies per step split by request index over %d GPU(s) (%d per GPU), "
                               "fixed %d-byte serialized requests, 5 %% invalid, accept bytes gathered to host and "
@@ -780,6 +840,7 @@ def main():
         "config": config,
         "roofline": roofline,
         "verdicts_as_expected": verdicts_ok,
+        **({"multi_gpu": out_multi} if world > 1 else {}),
         "timing": {"mode": "pipelined (prep of step k+1 beside main of step k)" if args.pipeline else "sequential",
                    "reps_s": reps, "median_of": len(reps), "warmup_steps_run": warm_steps,
                    "kernel_sum_ms": path_ms, "gap_ms_per_step": ms_step - path_ms * n / pn,
@@ -804,7 +865,7 @@ def main():
         out["cpu_baseline"] = cb
         if cb:
             out["gpu_over_cpu"] = value / cb["value"]
-            out["gpu_over_cpu_share"] = value / cb["share_verifies_per_s"]
+            out["gpu_over_cpu_full_socket_projection"] = value / cb["full_socket_projection_verifies_per_s"]
     print(json.dumps(out), flush=True)
     rdv.close()
 

@@ -210,6 +210,24 @@ int edv_sync(int device);
 int edv_device_count(void);
 
 /*
+ * Device placement on a multi-GPU node.  edv_verify_batch / edv_sha256_batch
+ * split a batch only into shards of at least 65,536 requests (one wave per SIMD
+ * of a whole MI355X: a smaller shard takes as long as a full one; EDV_MIN_SHARD
+ * overrides), so a Node-sized batch (a prod of a few hundred requests, or one
+ * Verifier.verify) runs whole on ONE device, on the calling thread, and no
+ * other device is initialised.  That device is edv_pick_device's choice among
+ * device_mask (0 = all): an initialised device with nothing in flight, else a
+ * device not yet initialised (order starting at pid mod devices), else the
+ * least-loaded one.  The Node's asynchronous path asks it for the device of
+ * each submission (edv_verify_batch_async takes the device explicitly).
+ * edv_context_count: devices whose context (streams, scratch, B table) exists.
+ * Reference: the per-request call being placed, nacl_wrappers.py:232-242, made
+ * per prod (plenum/server/node.py:1026-1049, stp_core/config.py:28).
+ */
+int edv_pick_device(uint32_t device_mask);
+int edv_context_count(void);
+
+/*
  * The shard split edv_verify_batch uses (host only, no GPU needed): bounds[0..g]
  * with shard k = requests [bounds[k], bounds[k+1]).  Equal request counts
  * (n*k/g) when every message has the same SHA-512 block count; otherwise equal

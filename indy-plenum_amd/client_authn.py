@@ -371,6 +371,13 @@ class CoreAuthMixin:
                     or cls.getVerkey is not SimpleAuthNr.getVerkey
                     or base58._native is None)
 
+    def device_digests_ok(self):
+        """Device request digests (digest_is_signing_bytes in csrc/edv_host.cpp)
+        treat exactly signature / signatures / fees as the keys outside the
+        signing bytes, i.e. the stock excluded_from_signing (client_authn.py:174);
+        with any other set the signing bytes are not signingState's bytes."""
+        return set(self.excluded_from_signing) == CoreAuthMixin.excluded_from_signing
+
     def _native_prep(self, reqs, verifier):
         """_edvhost.prep_core_batch for the stock authenticator, else None."""
         if not self._stock(verifier):
@@ -398,7 +405,8 @@ class CoreAuthMixin:
         if self._stock(verifier) and edv.native_batch_enabled():
             submit, wait = edv.async_addresses()
             h = _edvhost.auth_core_submit(reqs, self.clients, self.excluded_from_signing, submit, wait,
-                                          edv.BATCH_DEVICE, edv.PREP_THREADS, self._state_nyms(reqs), digests)
+                                          edv.batch_device(), edv.PREP_THREADS, self._state_nyms(reqs),
+                                          digests and self.device_digests_ok())
             return PendingAuth(lambda: self._finish_native(reqs, h, verifier))
         out = self.authenticate_batch(reqs, verifier)
         return PendingAuth(lambda: (out, [None] * len(reqs)))
@@ -445,6 +453,12 @@ class CoreAuthMixin:
                 i = r.get(IDENTIFIER)
                 if type(i) is str and i and i not in seen and not clients.get(i):
                     seen.add(i)
+                    try:
+                        i.encode()
+                    except UnicodeEncodeError:
+                        # e.g. a lone surrogate: that request alone takes the plan,
+                        # whose getVerkey raises the reference's error for it
+                        continue
                     idrs.append(i)
         if not idrs:
             return None
@@ -456,9 +470,14 @@ class CoreAuthMixin:
         out = {}
         loads = json.loads
         for i, key in zip(idrs, keys):
-            data = state.get(key, False)
-            if not data:
-                continue
+            try:
+                data = state.get(key, False)
+                if not data:
+                    continue
+            except MemoryError:
+                raise
+            except Exception:
+                continue  # a read that raises: the plan repeats it for that request alone
             try:
                 nym = loads(bytes(data).decode() if isinstance(data, (bytes, bytearray)) else data)
             except Exception:

@@ -707,14 +707,39 @@ struct Batch {
   std::vector<Py_ssize_t> todo;
   // asynchronous submission (auth_core_submit): the batch is in flight until waited for
   bool pending = false;
+  // the wait for the device call failed: every later finish raises again (the
+  // arena's verdict bytes are not the device's), and the arena is never reused
+  // (a device slot may still reference it)
+  bool failed = false;
   int device = 0;
   int64_t ticket = -1;
   wait_fn_t wait = nullptr;
   ~Batch() {
     for (FastItem& it : items) { Py_DECREF(it.idr); Py_DECREF(it.sig_o); Py_DECREF(it.vk_o); }
-    if (ar) g_arenas.push_back(ar);
+    if (ar && !failed) g_arenas.push_back(ar);  // failed: leaked on purpose
   }
 };
+
+// Wait for a submitted batch (GIL released).  0 = verdicts are in the arena;
+// else the batch is marked failed, for good, and a Python error is set.
+int finish_wait(Batch& b) {
+  if (b.failed) {
+    PyErr_SetString(PyExc_RuntimeError, "edv_wait_async failed earlier for this batch");
+    return -1;
+  }
+  if (!b.pending) return 0;
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = b.wait(b.device, b.ticket);
+  Py_END_ALLOW_THREADS
+  b.pending = false;
+  if (rc != 0) {
+    b.failed = true;
+    PyErr_Format(PyExc_RuntimeError, "edv_wait_async failed (%d)", rc);
+    return -1;
+  }
+  return 0;
+}
 
 // Request.getDigest (request.py:71-72) hashes the serialization of signingState =
 // {identifier, reqId, operation[, protocolVersion if not None]} (request.py:77-87);
@@ -883,6 +908,7 @@ int pack_all(Batch& b, int threads) {
   }
   memcpy(base + b.o_off, b.moff.data(), 8 * (nf + 1));
   memset(base + b.o_msg + b.msgs.size(), 0, 64);
+  memset(base + b.o_acc, 0, nf);  // reject until the device writes a verdict (arenas are reused)
   Py_END_ALLOW_THREADS
   return 0;
 }
@@ -1030,9 +1056,11 @@ void batch_capsule_free(PyObject* cap) {
   Batch* b = static_cast<Batch*>(PyCapsule_GetPointer(cap, kBatchCapsule));
   if (!b) { PyErr_Clear(); return; }
   if (b->pending && b->wait) {
+    int rc;
     Py_BEGIN_ALLOW_THREADS
-    (void)b->wait(b->device, b->ticket);  // the device may still write into the arena
+    rc = b->wait(b->device, b->ticket);  // the device may still write into the arena
     Py_END_ALLOW_THREADS
+    if (rc != 0) b->failed = true;       // keep the arena out of the free list
   }
   delete b;
 }
@@ -1081,18 +1109,15 @@ PyObject* py_auth_core_submit(PyObject*, PyObject* args) {
 PyObject* py_auth_core_finish(PyObject*, PyObject* cap) {
   Batch* b = static_cast<Batch*>(PyCapsule_GetPointer(cap, kBatchCapsule));
   if (!b) return nullptr;
-  if (b->pending) {
-    int rc;
-    Py_BEGIN_ALLOW_THREADS
-    rc = b->wait(b->device, b->ticket);
-    Py_END_ALLOW_THREADS
-    b->pending = false;
-    if (rc != 0) {
-      PyErr_Format(PyExc_RuntimeError, "edv_wait_async failed (%d)", rc);
-      return nullptr;
-    }
-  }
-  return build_output(*b, b->want_dig);
+  if (finish_wait(*b) < 0) return nullptr;
+  if (b->want_dig) return build_output(*b, true);
+  // (out, slow, rejected, None): the documented shape without digests too
+  PyObject* r3 = build_output(*b, false);
+  if (!r3) return nullptr;
+  PyObject* r4 = Py_BuildValue("(OOOO)", PyTuple_GET_ITEM(r3, 0), PyTuple_GET_ITEM(r3, 1), PyTuple_GET_ITEM(r3, 2),
+                               Py_None);
+  Py_DECREF(r3);
+  return r4;
 }
 
 // ---- ReqAuthenticator.authenticate_batch_submit for the single stock
@@ -1208,17 +1233,7 @@ PyObject* py_req_auth_finish(PyObject*, PyObject* args) {
     PyErr_SetString(PyExc_TypeError, "not a req_auth_submit handle");
     return nullptr;
   }
-  if (b->pending) {
-    int rc;
-    Py_BEGIN_ALLOW_THREADS
-    rc = b->wait(b->device, b->ticket);
-    Py_END_ALLOW_THREADS
-    b->pending = false;
-    if (rc != 0) {
-      PyErr_Format(PyExc_RuntimeError, "edv_wait_async failed (%d)", rc);
-      return nullptr;
-    }
-  }
+  if (finish_wait(*b) < 0) return nullptr;
   const size_t nf = b->items.size();
   const uint8_t* acc = nf ? b->ar->p + b->o_acc : nullptr;
   const int gc_was = gc_pause_for(b->n_all);
@@ -1400,6 +1415,16 @@ int scan_flat_json(const uint8_t* p, size_t n, const uint8_t** vk, size_t* vk_n,
   return i == n ? 1 : 0;
 }
 
+// An ordinary exception raised for one identifier (not KeyboardInterrupt /
+// SystemExit / MemoryError): cleared, and the identifier is left out.
+bool skippable_error() {
+  if (PyErr_ExceptionMatches(PyExc_Exception) && !PyErr_ExceptionMatches(PyExc_MemoryError)) {
+    PyErr_Clear();
+    return true;
+  }
+  return false;
+}
+
 PyObject* py_state_nyms(PyObject*, PyObject* args) {
   PyObject *reqs, *clients, *state_get, *json_loads;
   if (!PyArg_ParseTuple(args, "OO!OO", &reqs, &PyDict_Type, &clients, &state_get, &json_loads)) return nullptr;
@@ -1430,7 +1455,13 @@ PyObject* py_state_nyms(PyObject*, PyObject* args) {
     }
     Py_ssize_t ulen;
     const char* u = PyUnicode_AsUTF8AndSize(idr, &ulen);
-    if (!u) goto fail;
+    // an identifier that cannot be encoded (a lone surrogate is valid json.loads
+    // output) or whose state read raises: skipped, so that request alone takes the
+    // Python plan, whose getVerkey raises the reference's error for it alone
+    if (!u) {
+      if (!skippable_error()) goto fail;
+      continue;
+    }
     // nym_to_state_key: sha256(identifier.encode()), the kernel's SHA-256 on the CPU
     buf.assign(size_t(ulen) + 48, 0);
     memcpy(buf.data() + 16, u, size_t(ulen));
@@ -1447,11 +1478,14 @@ PyObject* py_state_nyms(PyObject*, PyObject* args) {
     if (!kb) goto fail;
     PyObject* data = PyObject_CallFunctionObjArgs(state_get, kb, Py_False, nullptr);
     Py_DECREF(kb);
-    if (!data) goto fail;
+    if (!data) {
+      if (!skippable_error()) goto fail;
+      continue;
+    }
     const int truth = PyObject_IsTrue(data);
     if (truth <= 0) {
       Py_DECREF(data);
-      if (truth < 0) goto fail;
+      if (truth < 0 && !skippable_error()) goto fail;
       continue;
     }
     const uint8_t* txt = nullptr;

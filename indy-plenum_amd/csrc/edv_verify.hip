@@ -21,8 +21,10 @@
 #include <string.h>
 #include <stdlib.h>
 #include <stdio.h>
+#include <atomic>
 #include <mutex>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 #include <string>
 
@@ -421,6 +423,8 @@ struct ChunkBufs {
 struct DevCtx {
   std::mutex mu;
   bool ready = false;
+  std::atomic<bool> live{false};   // ready, readable without mu (placement, edv_context_count)
+  std::atomic<int> inflight{0};    // calls running here + async batches not yet completed
   int dev = -1;                    // logical device (edv_* device index)
   int phys = -1;                   // HIP device it runs on
   hipStream_t stream = nullptr;    // the library stream (edv_stream)
@@ -460,6 +464,9 @@ struct DevCtx {
   AsyncSlot as[kAsyncSlots];
   hipStream_t hac = nullptr;
   int64_t next_ticket = 0;
+  // tickets whose wait failed: their slot drops them (nothing is copied into the
+  // caller's buffers afterwards) and every later wait for them fails again
+  std::vector<int64_t> failed_tickets;
   DevBuf sigs, pks, msgs, off, acc;
   PinnedBuf stage[kQ], acc_host;
   // Pipelined submission (edv_verify_batch_dev_pipelined): two state sets, a
@@ -538,6 +545,7 @@ int ctx_init(DevCtx& c) {
     c.btab_built = true;
   }
   c.ready = true;
+  c.live.store(true);
   return 0;
 }
 
@@ -1028,12 +1036,27 @@ int run_digest_shard(DevCtx& c, const uint8_t* msgs, const uint64_t* off, uint64
 }
 
 // Asynchronous host path.  Wait for a slot's batch and hand over its verdicts.
-int async_complete(DevCtx::AsyncSlot& s) {
+void async_fail(DevCtx& c, DevCtx::AsyncSlot& s) {
+  if (c.failed_tickets.size() >= 256) c.failed_tickets.erase(c.failed_tickets.begin());
+  c.failed_tickets.push_back(s.ticket);
+  s.ticket = -1;
+  c.inflight.fetch_sub(1);
+}
+bool ticket_failed(const DevCtx& c, int64_t t) {
+  for (int64_t x : c.failed_tickets)
+    if (x == t) return true;
+  return false;
+}
+int async_complete(DevCtx& c, DevCtx::AsyncSlot& s) {
   if (s.ticket < 0) return 0;
-  HIPOK(hipEventSynchronize(s.done), "async wait");
+  if (const hipError_t e = hipEventSynchronize(s.done); e != hipSuccess) {
+    async_fail(c, s);
+    return set_err(EDV_E_HIP, "async wait", e);
+  }
   if (!s.acc_pinned) memcpy(s.accept, s.acc_host.p, s.n);
   if (s.digests && !s.dig_pinned) memcpy(s.digests, s.dig_host.p, 32 * s.n);
   s.ticket = -1;
+  c.inflight.fetch_sub(1);
   return 0;
 }
 
@@ -1048,7 +1071,7 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
   const int64_t t = c.next_ticket;
   DevCtx::AsyncSlot& s = c.as[t % kAsyncSlots];
   int err;
-  if ((err = async_complete(s))) return err;  // the batch of kAsyncSlots submissions ago
+  if ((err = async_complete(c, s))) return err;  // the batch of kAsyncSlots submissions ago
   const uint64_t mbase = off[0], mbytes = off[n] - mbase;
   if (s.sigs.ensure(n * 64) || s.pks.ensure(n * 32) || s.msgs.ensure(mbytes + 64) || s.off.ensure((n + 1) * 8) ||
       s.acc.ensure(n) || (digests && s.dig.ensure(32 * n)))
@@ -1103,6 +1126,7 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
     HIPOK(hipMemcpyAsync(h_dig, d_dig, 32 * n, hipMemcpyDeviceToHost, ks), "d2h digests");
   }
   HIPOK(hipEventRecord(s.done, ks), "record");
+  c.inflight.fetch_add(1);
   s.ticket = t;
   s.accept = accept;
   s.digests = digests;
@@ -1141,10 +1165,54 @@ void shard_bounds(const uint64_t* off, uint64_t n, uint32_t g, uint64_t* b) {
   while (k < g) b[k++] = n;
 }
 
-// Validate a host batch and split [0, n) over the devices of device_mask, one
-// host thread per device; shard(ctx, lo, hi) does the work under the context lock.
-template <class Shard>
-int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard shard) {
+// ---- device placement (several GPUs in one process)
+// A shard smaller than one wave per SIMD of a whole MI355X (256 CUs x 4 SIMDs x
+// 64 lanes) takes as long as a full one: prep and main run one serial chain per
+// lane and a lane's latency, not the lane count, sets the time (profiles/r03/
+// e2e_host_parts_s36.jsonl, profiles/r04/latency_vs_n_*.jsonl).  So a batch is
+// split only into shards of at least that many requests; a smaller batch (a
+// Node's prod: a few hundred, or a single Verifier.verify) runs whole on ONE
+// device, with no thread spawned and no other device touched.
+// EDV_MIN_SHARD overrides (tests split small batches on purpose).
+constexpr uint64_t kMinShard = 65536;
+uint64_t min_shard() {
+  static const uint64_t v = [] {
+    if (const char* e = getenv("EDV_MIN_SHARD")) {
+      const long long x = strtoll(e, nullptr, 10);
+      if (x >= 1) return uint64_t(x);
+    }
+    return kMinShard;
+  }();
+  return v;
+}
+
+// The device for a batch that runs on one device, among `devs`: an initialised
+// device with nothing in flight (the lowest-loaded initialised one first, so a
+// process that verifies one batch at a time stays on one context); if every
+// initialised device is busy, a device not yet initialised (in an order that
+// starts at pid mod ndev, so the processes of a node spread over its GPUs);
+// else the least-loaded device.
+int pick_device(const std::vector<int>& devs) {
+  const int k = int(devs.size());
+  if (k == 1) return devs[0];
+  const int start = int(uint64_t(getpid()) % uint64_t(k));
+  int best = -1, best_load = 0;
+  for (int j = 0; j < k; j++) {
+    const int d = devs[(start + j) % k];
+    if (!g_ctx[d]->live.load()) continue;
+    const int load = g_ctx[d]->inflight.load();
+    if (best < 0 || load < best_load) { best = d; best_load = load; }
+  }
+  if (best >= 0 && best_load == 0) return best;
+  for (int j = 0; j < k; j++) {
+    const int d = devs[(start + j) % k];
+    if (!g_ctx[d]->live.load()) return d;
+  }
+  if (best >= 0) return best;
+  return devs[start];
+}
+
+std::vector<int> devices_of(uint32_t device_mask, int* err) {
   int ndev;
   {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -1153,16 +1221,38 @@ int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard 
   std::vector<int> devs;
   for (int d = 0; d < ndev && d < 32; d++)
     if (device_mask == 0 || (device_mask >> d) & 1u) devs.push_back(d);
-  if (devs.empty()) return set_err(EDV_E_NODEV, "no device selected / visible");
-  const uint32_t g = uint32_t(devs.size());
-  std::vector<uint64_t> bounds(g + 1);
-  shard_bounds(off, n, g, bounds.data());
+  *err = devs.empty() ? set_err(EDV_E_NODEV, "no device selected / visible") : 0;
+  return devs;
+}
+
+// Counts a call as in flight on its device while it runs.
+struct Inflight {
+  DevCtx* c;
+  explicit Inflight(DevCtx* x) : c(x) { c->inflight.fetch_add(1); }
+  ~Inflight() { c->inflight.fetch_sub(1); }
+};
+
+// Validate a host batch and split [0, n) over the devices of device_mask (at
+// most one shard per min_shard() requests), one host thread per shard; a batch
+// that is one shard runs on the calling thread on pick_device's device.
+// shard(ctx, lo, hi) does the work under the context lock.
+template <class Shard>
+int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard shard) {
+  int err;
+  std::vector<int> devs = devices_of(device_mask, &err);
+  if (err) return err;
+  const uint64_t most = n / min_shard();
+  const uint32_t g = uint32_t(most < devs.size() ? (most > 1 ? most : 1) : devs.size());
   auto one = [&](int dev, uint64_t lo, uint64_t hi) {
+    Inflight inf(g_ctx[dev]);
     CtxLock cl(dev);
     if (cl.err) return cl.err;
     return shard(*cl.c, lo, hi);
   };
-  if (g == 1) return one(devs[0], 0, n);
+  if (g == 1) return one(pick_device(devs), 0, n);
+  devs.resize(g);
+  std::vector<uint64_t> bounds(g + 1);
+  shard_bounds(off, n, g, bounds.data());
   std::vector<int> rc(g, 0);
   std::vector<std::string> errs(g);
   std::vector<std::thread> th;
@@ -1196,8 +1286,12 @@ int check_dev_align(const void* d_sigs, const void* d_pks, const void* d_off) {
 // ------------------------------------------------------------------ C-ABI
 extern "C" {
 
-#ifdef EDV_MEASURE_NO_VERIFY
+// Builds whose verdicts are not libsodium's say so in their version string;
+// edv.lib() refuses them unless EDV_ALLOW_MEASUREMENT_LIB=1.
+#if defined(EDV_MEASURE_NO_VERIFY)
 const char* edv_version(void) { return "edv 0.2.0 gfx950 MEASUREMENT-ONLY: verification skipped"; }
+#elif defined(EDV_AB_SIDES)
+const char* edv_version(void) { return "edv 0.2.0 gfx950 MEASUREMENT-ONLY: prep sides subset, wrong verdicts"; }
 #else
 const char* edv_version(void) { return "edv 0.2.0 gfx950"; }
 #endif
@@ -1206,6 +1300,22 @@ const char* edv_last_error(void) { return g_err.c_str(); }
 int edv_device_count(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   return device_count_locked();
+}
+
+int edv_context_count(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int n = device_count_locked();
+  int k = 0;
+  for (int d = 0; d < n; d++) k += g_ctx[d]->live.load() ? 1 : 0;
+  return k;
+}
+
+int edv_pick_device(uint32_t device_mask) {
+  g_err.clear();
+  int err;
+  const std::vector<int> devs = devices_of(device_mask, &err);
+  if (err) return err;
+  return pick_device(devs);
 }
 
 int edv_shard_split(const uint64_t* msg_off, uint64_t n, uint32_t g, uint64_t* bounds) {
@@ -1267,6 +1377,7 @@ int edv_wait_async(int device, int64_t ticket) {
   CtxLock cl(device);
   if (cl.err) return cl.err;
   if (ticket < 0 || ticket >= cl.c->next_ticket) return set_err(EDV_E_ARG, "unknown ticket");
+  if (ticket_failed(*cl.c, ticket)) return set_err(EDV_E_HIP, "async batch failed earlier");
   for (auto& s : cl.c->as) {
     if (s.ticket != ticket) continue;
     // wait without holding the device lock (other threads keep submitting);
@@ -1275,10 +1386,15 @@ int edv_wait_async(int device, int64_t ticket) {
     cl.lk.unlock();
     const hipError_t e = hipEventSynchronize(done);
     cl.lk.lock();
-    if (e != hipSuccess) return set_err(EDV_E_HIP, "async wait", e);
-    return s.ticket == ticket ? async_complete(s) : 0;
+    if (e != hipSuccess) {
+      if (s.ticket == ticket) async_fail(*cl.c, s);
+      return set_err(EDV_E_HIP, "async wait", e);
+    }
+    return s.ticket == ticket ? async_complete(*cl.c, s) : 0;
   }
-  return 0;  // already complete (waited for, or its slot was reused)
+  // already complete (waited for, or its slot was reused) -- unless it failed meanwhile
+  if (ticket_failed(*cl.c, ticket)) return set_err(EDV_E_HIP, "async batch failed earlier");
+  return 0;
 }
 
 int edv_sha256_batch(const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, uint8_t* out, uint32_t device_mask) {

@@ -230,8 +230,10 @@ EDV_HD int w8_bitlen(const uint32_t a[8]) {
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const uint32_t x = a[i];
-#if defined(__HIP_DEVICE_COMPILE__)
-    const int lz = __builtin_clz(x);  // v_ffbh_u32; masked off for x == 0
+    // zero-defined form (32 for x == 0: v_ffbh_u32 + v_min_u32), so no poison
+    // value can reach the window count that bounds the main loop
+#if defined(__clang__)
+    const int lz = __builtin_clzg(x, 32);
 #else
     const int lz = x ? __builtin_clz(x) : 32;
 #endif

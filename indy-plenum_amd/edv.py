@@ -22,6 +22,7 @@ from . import _edvhost  # native host-side packing (csrc/edv_host.cpp, row f-1)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("EDV_LIB", os.path.join(_HERE, "libedv.so"))
+MEASUREMENT_TAG = "MEASUREMENT-ONLY"  # in edv_version() of builds whose verdicts are not libsodium's
 
 EDV_OK = 0
 EDV_E_ARG = -1
@@ -59,6 +60,15 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise EdvUnavailable("libedv.so not built at {} (run __graft_entry__.build())".format(LIB_PATH))
         h = ctypes.CDLL(LIB_PATH)
+        h.edv_version.restype = ctypes.c_char_p
+        ver = h.edv_version().decode(errors="replace")
+        if MEASUREMENT_TAG in ver and os.environ.get("EDV_ALLOW_MEASUREMENT_LIB") != "1":
+            # a measurement build (e.g. variants/libedv_noverify.so reports every
+            # signature valid) must never authenticate requests: fail closed,
+            # as the reference's Verifier never returns True without libsodium's
+            # check (nacl_wrappers.py:232-242)
+            raise EdvUnavailable("{} is a measurement-only build ({}); refusing to load it "
+                                 "(EDV_ALLOW_MEASUREMENT_LIB=1 is for benchmarks only)".format(LIB_PATH, ver))
         vp, u64 = ctypes.c_void_p, ctypes.c_uint64
         h.edv_verify_batch.argtypes = [vp, vp, vp, vp, u64, vp, ctypes.c_uint32]
         h.edv_verify_batch.restype = ctypes.c_int
@@ -105,6 +115,10 @@ def lib():
         h.edv_host_free.restype = ctypes.c_int
         h.edv_device_count.argtypes = []
         h.edv_device_count.restype = ctypes.c_int
+        h.edv_context_count.argtypes = []
+        h.edv_context_count.restype = ctypes.c_int
+        h.edv_pick_device.argtypes = [ctypes.c_uint32]
+        h.edv_pick_device.restype = ctypes.c_int
         h.edv_dev_alloc.argtypes = [ctypes.c_int, u64, ctypes.POINTER(ctypes.c_void_p)]
         h.edv_dev_free.argtypes = [ctypes.c_int, vp]
         h.edv_h2d.argtypes = [ctypes.c_int, vp, vp, u64]
@@ -121,6 +135,27 @@ def version() -> str:
 
 def device_count() -> int:
     return lib().edv_device_count()
+
+
+def context_count() -> int:
+    """Devices whose context the library has initialised (placement tests)."""
+    return lib().edv_context_count()
+
+
+def pick_device(device_mask: int = 0) -> int:
+    """The device edv_pick_device chooses for a one-device batch (include/edv.h)."""
+    d = lib().edv_pick_device(device_mask)
+    if d < 0:
+        _check(d)
+    return d
+
+
+def batch_device() -> int:
+    """Device of the next native asynchronous whole-batch submission: BATCH_DEVICE
+    if set, else the library's choice among BATCH_DEVICE_MASK (an idle
+    initialised device, else a fresh one), so the Nodes of one process spread
+    over the GPUs while a lone caller stays on one context."""
+    return BATCH_DEVICE if BATCH_DEVICE is not None else pick_device(BATCH_DEVICE_MASK)
 
 
 def stream(device: int = 0) -> int:
@@ -309,7 +344,7 @@ def async_addresses():
     return _async_addrs
 
 
-BATCH_DEVICE = 0               # device of the native asynchronous whole-batch path
+BATCH_DEVICE = None            # device of the native asynchronous whole-batch path (None: batch_device())
 
 
 def sha256_address() -> int:

@@ -180,8 +180,8 @@ class ReqAuthenticator:
             return None
         submit, wait = edv.async_addresses()
         with gc_paused_for(len(reqs)):
-            h = _edvhost.req_auth_submit(reqs, a.clients, a.excluded_from_signing, submit, wait, edv.BATCH_DEVICE,
-                                         edv.PREP_THREADS, a._state_nyms(reqs), digests,
+            h = _edvhost.req_auth_submit(reqs, a.clients, a.excluded_from_signing, submit, wait, edv.batch_device(),
+                                         edv.PREP_THREADS, a._state_nyms(reqs), digests and a.device_digests_ok(),
                                          (a.query_types, a.write_types, cls.action_types))
 
         def finish():

@@ -29,6 +29,13 @@ def _rank(rank, world, token, q):
         # this shard's verdicts: the C3 damage pattern, as a rank's accept bytes would be
         acc = np.ones(hi - lo, np.uint8)
         acc[workload.damage_positions(lo, hi - lo, 20)] = 0
+        # rank 0 alone (the one-GPU same-workload reference), then all ranks
+        import time as _t
+        own = []
+        alone = bench.timed_steps(lambda: _t.sleep(0.02), lambda: None, 3, 1, rdv, only_rank=0, own=own)
+        joint = bench.timed_steps(lambda: _t.sleep(0.01 * (rank + 1)), lambda: None, 2, 2, rdv, own=own)
+        assert alone[0] >= 0.06 and (rank == 0) == (own[0] >= 0.06)
+        assert all(j >= 0.02 * world for j in joint) and all(o >= 0.02 * (rank + 1) for o in own[1:])
         parts = rdv.gather(acc.tobytes(), broadcast=False)
         allv = rdv.gather(b"r%d" % rank)
         rdv.barrier()
@@ -95,3 +102,24 @@ def test_bench_imports_no_torch():
     r = subprocess.run([sys.executable, "-c", "import json; " + code], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     assert json.loads(r.stdout.strip()) is False
+
+
+@pytest.mark.parametrize("vis,local,world,want", [
+    (None, 3, 8, (0, "3")), ("4,5,6,7", 2, 4, (0, "6")), (" 0 , 1", 1, 2, (0, "1")),
+    ("", 1, 2, (1, None)), ("0", 0, 1, (0, None))])
+def test_each_rank_sees_only_its_gpu(monkeypatch, vis, local, world, want):
+    """N > 1: every rank narrows HIP_VISIBLE_DEVICES to its LOCAL_RANK-th device
+    before the HIP runtime loads, so it initialises one GPU;
+    not under EDV_VIRTUAL_DEVICES (ranks share logical devices of one GPU)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.delenv("EDV_VIRTUAL_DEVICES", raising=False)
+    if vis is None:
+        monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    else:
+        monkeypatch.setenv("HIP_VISIBLE_DEVICES", vis)
+    assert bench.narrow_to_own_gpu(local, world) == want
+    if want[1] is not None:
+        assert os.environ["HIP_VISIBLE_DEVICES"] == want[1]
+    monkeypatch.setenv("EDV_VIRTUAL_DEVICES", "8")
+    assert bench.narrow_to_own_gpu(5, 8) == (5, None)

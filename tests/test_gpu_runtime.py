@@ -357,7 +357,9 @@ def test_multi_device_path_on_virtual_devices():
     one-GPU box): one host thread and context per device, shards by index (C2
     lengths: equal counts) checked against libsodium's committed verdict bitmask,
     and by estimated cost (C4 lengths) against the checker."""
-    env = dict(os.environ, EDV_VIRTUAL_DEVICES="4", ROOT=ROOT)
+    # EDV_MIN_SHARD: the 30,000-request C4 batch is split too (below the default
+    # 65,536-request minimum shard it would run whole on one device)
+    env = dict(os.environ, EDV_VIRTUAL_DEVICES="4", EDV_MIN_SHARD="4096", ROOT=ROOT)
     r = subprocess.run([sys.executable, "-c", _VIRTUAL], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
@@ -366,6 +368,89 @@ def test_multi_device_path_on_virtual_devices():
     assert out["c3_bounds"] == [0, 65536, 131072, 196608, 262144]
     assert out["c4_bounds"] == out["c4_bounds_restated"]
     assert out["bad_mask"] == "EdvUnavailable"
+
+
+_PLACEMENT = r"""
+import json, os, statistics, sys, time
+import numpy as np
+sys.path.insert(0, os.environ["ROOT"]); sys.path.insert(0, os.path.join(os.environ["ROOT"], "tests"))
+import oracle_lib as orc
+from indy_plenum_amd import edv
+out = {"devices": edv.device_count(), "contexts0": edv.context_count()}
+sigs, pks, msgs, off = orc.corpus(0x91AC, 0, 400, mode=0, invalid_permille=100)
+want = np.frombuffer(orc.verify_batch(sigs.tobytes(), pks.tobytes(), msgs.tobytes(), off, 400, 8), np.uint8)
+def lat(k, reps=40):
+    o = off[:k + 1]
+    got = edv.verify_arrays(sigs[:64 * k], pks[:32 * k], msgs, o)
+    assert np.array_equal(got, want[:k])
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        edv.verify_arrays(sigs[:64 * k], pks[:32 * k], msgs, o)
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts)
+out["lat1_s"] = lat(1)
+out["contexts_after_1"] = edv.context_count()
+out["lat400_s"] = lat(400)
+out["contexts_after_400"] = edv.context_count()
+# asynchronous submissions in flight together spread over devices; one at a time they stay put
+acc = [np.zeros(400, np.uint8) for _ in range(4)]
+picks, tickets = [], []
+for a in acc:
+    d = edv.pick_device()
+    picks.append(d)
+    tickets.append((d, edv.verify_async(sigs, pks, msgs, off, a, device=d)))
+for d, t in tickets:
+    edv.wait_async(t, device=d)
+out["async_spread"] = len(set(picks))
+out["async_equal"] = all(np.array_equal(a, want) for a in acc)
+seq = []
+for _ in range(5):
+    d = edv.pick_device()
+    seq.append(d)
+    edv.wait_async(edv.verify_async(sigs, pks, msgs, off, acc[0], device=d), device=d)
+out["async_sequential_devices"] = len(set(seq))
+out["contexts_after_async"] = edv.context_count()
+if out["devices"] == 8:
+    # C3-shaped: 8 x 65,536 requests split 8 ways, against libsodium's committed bitmask
+    meta = json.load(open(os.path.join(os.environ["ROOT"], "tests", "golden", "corpus_bitmask.json")))
+    cfg = meta["corpora"]["c2_256B"]
+    n = 8 * 65536
+    s3, p3, m3, o3 = orc.corpus(cfg["seed"], 0, n, cfg["mode"], cfg["invalid_permille"])
+    bits = np.fromfile(os.path.join(os.environ["ROOT"], "tests", "golden", "corpus_c2_256B.bits"), np.uint8)
+    out["c3_equal"] = bool(np.array_equal(edv.verify_arrays(s3, p3, m3, o3), np.unpackbits(bits[:n // 8], bitorder="little")))
+    out["contexts_after_c3"] = edv.context_count()
+print(json.dumps(out))
+"""
+
+
+def _placement(vdev):
+    env = dict(os.environ, EDV_VIRTUAL_DEVICES=str(vdev), ROOT=ROOT)
+    env.pop("EDV_MIN_SHARD", None)
+    r = subprocess.run([sys.executable, "-c", _PLACEMENT], env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_device_placement_node_sized_batches():
+    """VERDICT r3 next #3, on eight logical devices of this one GPU
+    (EDV_VIRTUAL_DEVICES=8): a 1-request and a 400-request edv_verify_batch
+    initialise exactly ONE device context (no thread per device, no empty
+    shard), and their median latency does not grow against one logical device;
+    asynchronous batches in flight together spread over devices, one at a time
+    they stay on one; a C3-shaped 8 x 65,536 batch still splits 8 ways, with
+    libsodium's committed verdicts."""
+    one = _placement(1)
+    eight = _placement(8)
+    assert eight["devices"] == 8 and one["devices"] == 1
+    assert eight["contexts0"] == 0
+    assert eight["contexts_after_1"] == 1 and eight["contexts_after_400"] == 1
+    assert eight["async_equal"] and one["async_equal"]
+    assert eight["async_spread"] >= 2 and eight["async_sequential_devices"] == 1
+    assert eight["c3_equal"] and eight["contexts_after_c3"] == 8
+    for k in ("lat1_s", "lat400_s"):
+        assert eight[k] <= 1.25 * one[k] + 1e-4, (k, eight[k], one[k])
+    print(json.dumps({"placement_1dev": one, "placement_8dev": eight}))
 
 
 def _bench(args, env=None, launcher=None, timeout=420):
@@ -429,6 +514,13 @@ def test_bench_two_gpus_launched_by_bench():
     assert line["n_gpus"] == 2 and line["verdicts_as_expected"] is True
     assert line["config"]["workload"].startswith("C3") and line["config"]["per_gpu"] == 524288
     assert line["timing"]["launch"] == "ranks started by bench.py"
+    # the fields a scaling curve needs
+    mg = line["multi_gpu"]
+    assert len(mg["per_rank_s"]) == 2 and mg["slowest_rank"] in (0, 1)
+    assert mg["slowest_rank_s"] == max(mg["per_rank_s"])
+    assert mg["one_gpu_same_workload_verifies_per_s"] > 1e6
+    assert abs(mg["scaling_efficiency"] - line["value"] / (2 * mg["one_gpu_same_workload_verifies_per_s"])) < 1e-9
+    assert mg["gpu_isolation"].startswith("EDV_VIRTUAL_DEVICES")
 
 
 def test_bench_two_gpus_under_torch_distributed_run():

@@ -465,6 +465,7 @@ def test_async_submit_finish_equals_sequential_with_digests(monkeypatch, with_st
     calls = []
     cbs, addrs, issued = _oracle_async_callbacks(calls)
     monkeypatch.setattr(edv, "async_addresses", lambda: addrs)
+    monkeypatch.setattr(edv, "BATCH_DEVICE", 0)
     monkeypatch.setattr(edv, "verify_address", lambda: addrs[0])
     monkeypatch.setattr(client_authn.CoreAuthMixin, "STATE_KEYS_ON_DEVICE", 10**9)
 
@@ -600,6 +601,7 @@ def test_native_req_auth_routing_edge_cases(monkeypatch):
     calls = []
     cbs, addrs, issued = _oracle_async_callbacks(calls)
     monkeypatch.setattr(edv, "async_addresses", lambda: addrs)
+    monkeypatch.setattr(edv, "BATCH_DEVICE", 0)
     monkeypatch.setattr(edv, "verify_address", lambda: addrs[0])
     monkeypatch.setattr(edv, "_OPEN_BATCH", H.oracle_open_batch)
     monkeypatch.setattr(edv, "open_batch", H.oracle_open_batch)
@@ -608,3 +610,104 @@ def test_native_req_auth_routing_edge_cases(monkeypatch):
     got = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in p.result()]
     assert got == want
     assert {o[1] for o in want if o[0] == "raise"} >= {"NoAuthenticatorFound", "AttributeError", "TypeError"}
+
+
+class _PickyState(_RecordingState):
+    """A state whose read raises for one key (that request alone fails)."""
+
+    def __init__(self, bad_key):
+        super().__init__()
+        self.bad_key = bad_key
+
+    def get(self, key, isCommitted=True):
+        if key == self.bad_key:
+            raise KeyError("corrupt node")
+        return super().get(key, isCommitted)
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_state_nyms_one_bad_identifier_fails_alone(monkeypatch, native):
+    """An identifier with a lone surrogate (valid json.loads output that cannot be
+    UTF-8 encoded) and an identifier whose state read raises, mixed into a batch
+    of good state-backed requests: every request gets exactly what the sequential
+    reference chain gives it -- the two odd ones their own exception, the rest
+    their identifiers -- instead of one exception failing the whole batch
+    (client_authn.py:148-160 -> domain_req_handler.py:158-167 per request)."""
+    import json
+    import hashlib
+    import test_authn_host as H
+    from indy_plenum_amd import client_authn, digest
+    from indy_plenum_amd.client_authn import CoreAuthNr, nym_to_state_key
+    signers = [H.Signer(seed=bytes([k + 9, 3]) * 16) for k in range(6)]
+    st = _PickyState(nym_to_state_key("BadRead1"))
+    auth = CoreAuthNr(state=st)
+    for s in signers:
+        st.kv[nym_to_state_key(s.identifier)] = json.dumps({"verkey": s.verkey, "role": None}).encode()
+    reqs = []
+    for i in range(60):
+        s = signers[i % len(signers)]
+        req = {"identifier": s.identifier, "reqId": i, "operation": {"type": "1", "n": i}, "protocolVersion": 2}
+        req["signature"] = s.sign(req)
+        reqs.append(req)
+    reqs[7] = {**reqs[7], "identifier": "Sur\ud800rogate"}
+    reqs[23] = {**reqs[23], "identifier": "BadRead1"}
+    with monkeypatch.context() as m:
+        m.setattr(edv, "open_batch", H.oracle_open_batch)
+        want = [H.outcome(lambda q=q: auth.authenticate(dict(q))) for q in reqs]
+    assert want[7][0] == "raise" and want[7][1] == "UnicodeEncodeError"
+    assert want[23][0] == "raise" and want[23][1] == "KeyError"
+    assert sum(w[0] == "ok" for w in want) == 58
+    if not native:
+        monkeypatch.setattr(client_authn, "_edvhost", None)
+    py = auth._state_nyms_py(reqs)
+    assert len(py) == len(signers)
+    calls = []
+    cb, addr = _oracle_verify_callback(calls)
+    monkeypatch.setattr(edv, "verify_address", lambda: addr)
+    monkeypatch.setattr(client_authn.CoreAuthMixin, "STATE_KEYS_ON_DEVICE", 1)
+    monkeypatch.setattr(digest, "nym_state_keys", lambda nyms, device_mask=0:
+                        [hashlib.sha256(x.encode()).digest() for x in nyms])
+    monkeypatch.setattr(edv, "_OPEN_BATCH", H.oracle_open_batch)
+    monkeypatch.setattr(edv, "open_batch", H.oracle_open_batch)
+    got = auth.authenticate_batch(reqs)
+    got = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in got]
+    assert got == want
+
+
+def test_failed_async_wait_stays_failed(monkeypatch):
+    """when the device wait of a submitted batch fails, result()
+    raises, and so does every later result()/digests() call -- the verdict bytes
+    in the (reused) arena are never read as verdicts -- and the arena is not
+    handed to the next batch.  The next batch still gets its own verdicts."""
+    import ctypes
+    import test_authn_host as H
+    from indy_plenum_amd import client_authn
+    sa, reqs = H.make_requests(300, seed=91)
+    with monkeypatch.context() as m:
+        m.setattr(edv, "open_batch", H.oracle_open_batch)
+        want = [H.outcome(lambda q=q: sa.authenticate(q)) for q in reqs]
+    calls = []
+    cbs, addrs, issued = _oracle_async_callbacks(calls)
+    WAIT = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.c_int64)
+    fail = {"on": True}
+
+    def bad_wait(device, ticket):
+        return -3 if fail["on"] else cbs[1](device, ticket)
+    bw = WAIT(bad_wait)
+    monkeypatch.setattr(edv, "async_addresses", lambda: (addrs[0], ctypes.cast(bw, ctypes.c_void_p).value))
+    monkeypatch.setattr(edv, "BATCH_DEVICE", 0)
+    monkeypatch.setattr(edv, "verify_address", lambda: addrs[0])
+    monkeypatch.setattr(client_authn.CoreAuthMixin, "STATE_KEYS_ON_DEVICE", 10**9)
+    monkeypatch.setattr(edv, "_OPEN_BATCH", H.oracle_open_batch)
+    monkeypatch.setattr(edv, "open_batch", H.oracle_open_batch)
+    p = sa.authenticate_batch_submit(reqs, digests=True)
+    for _ in range(3):
+        with pytest.raises(RuntimeError, match="edv_wait_async"):
+            p.result()
+    with pytest.raises(RuntimeError):
+        p.digests()
+    del p
+    fail["on"] = False
+    p2 = sa.authenticate_batch_submit(reqs, digests=False)
+    got = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in p2.result()]
+    assert got == want

@@ -123,6 +123,7 @@ def test_pool_overlap_on_the_native_async_path(monkeypatch):
     calls = []
     cbs, addrs, issued = _oracle_async_callbacks(calls)
     monkeypatch.setattr(edv, "async_addresses", lambda: addrs)
+    monkeypatch.setattr(edv, "BATCH_DEVICE", 0)
     monkeypatch.setattr(edv, "verify_address", lambda: addrs[0])
     monkeypatch.setattr(edv, "_OPEN_BATCH", H.oracle_open_batch)
     monkeypatch.setattr(edv, "open_batch", H.oracle_open_batch)

@@ -110,7 +110,7 @@ def run_isolated(mode, n, lib):
     measurement-only library that reports every request valid without running
     the verify kernels.  Same flood, same host path, same digests on the GPU."""
     import subprocess
-    env = dict(os.environ, EDV_LIB=lib)
+    env = dict(os.environ, EDV_LIB=lib, EDV_ALLOW_MEASUREMENT_LIB="1")  # this child only
     r = subprocess.run([sys.executable, os.path.abspath(__file__), "--mode", mode, "--n", str(n)],
                        capture_output=True, text=True, env=env, timeout=600)
     if r.returncode != 0:

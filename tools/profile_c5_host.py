@@ -128,6 +128,7 @@ def submit_bench(batch, n=4000, reps=20):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 20000
     edv.async_addresses = lambda: ADDRS
+    edv.BATCH_DEVICE = 0
     edv.verify_address = lambda: ADDRS[0]
     edv.native_batch_enabled = lambda: True
     if "--submit" in sys.argv:

@@ -8,7 +8,7 @@ for n in 65536 262144; do
 for v in 7 1 2 6 3; do
   L=indy-plenum_amd/variants/libedv_sides$v.so
   [ $v = 7 ] && L=indy-plenum_amd/libedv.so
-  EDV_LIB=$R/$L N=$n V=$v timeout -k 10 200 python3 - >> $O/sides.jsonl 2> $O/sides$v.err <<'PY' || { tail -20 $O/sides$v.err; exit 1; }
+  EDV_ALLOW_MEASUREMENT_LIB=1 EDV_LIB=$R/$L N=$n V=$v timeout -k 10 200 python3 - >> $O/sides.jsonl 2> $O/sides$v.err <<'PY' || { tail -20 $O/sides$v.err; exit 1; }
 import json, os, time
 from indy_plenum_amd import edv, workload
 n = int(os.environ["N"])

@@ -4,7 +4,7 @@ set -o pipefail
 O=gpurun_out/r02/s47
 mkdir -p $O
 for v in 7 1 2 6; do
-  EDV_LIB=indy-plenum_amd/variants/libedv_sides$v.so timeout -k 10 200 python3 - > $O/sides$v.json 2> $O/sides$v.err <<PY || { tail -20 $O/sides$v.err; exit 1; }
+  EDV_ALLOW_MEASUREMENT_LIB=1 EDV_LIB=indy-plenum_amd/variants/libedv_sides$v.so timeout -k 10 200 python3 - > $O/sides$v.json 2> $O/sides$v.err <<PY || { tail -20 $O/sides$v.err; exit 1; }
 import json, time
 from indy_plenum_amd import edv, workload
 b = workload.DeviceBatch(65536)
