@@ -1,0 +1,73 @@
+"""Synchronous edv_verify_batch on pinned host buffers at C2 (65,536 x 256 B):
+one sub-batch (the default) against Q sub-batches on Q streams, plain or each
+confined to its own 1/Q of the CUs (EDV_HOST_CUMASK modes 1-3, see
+host_streams in csrc/edv_verify.hip).  Median of R calls back to back, and of
+R calls 5 ms apart (the GPU idles in between, as a Node's calls would).
+Verdicts checked on every configuration.  Measurement only."""
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from indy_plenum_amd import edv, workload  # noqa: E402
+
+n = int(os.environ.get("N", 65536))
+R = int(os.environ.get("R", 21))
+b = workload.DeviceBatch(n, keep_host=True)
+sigs, pks, msgs, off = b.host_copy()
+want = b.expected()
+sizes = [sigs.nbytes, pks.nbytes, off.nbytes, msgs.nbytes, n]
+pb = edv.PinnedBuffer(sum(sizes) + 5 * 64)
+views, pos = [], 0
+for a, sz in zip((sigs, pks, off, msgs, None), sizes):
+    v = pb.array[pos:pos + sz]
+    if a is not None:
+        v[:] = a.view(np.uint8)
+    views.append(v)
+    pos += (sz + 63) // 64 * 64
+ps, pp, po, pm, pa = views
+po = po.view(np.uint64)
+lib = edv.lib()
+
+
+def call():
+    edv._check(lib.edv_verify_batch(ps.ctypes.data, pp.ctypes.data, pm.ctypes.data, po.ctypes.data, n,
+                                    pa.ctypes.data, 1))
+
+
+s = edv.stream(0)
+dev_ms = []
+for _ in range(R):
+    t = time.perf_counter()
+    b.verify(stream=s)
+    edv.sync(0)
+    dev_ms.append(1e3 * (time.perf_counter() - t))
+out = {"n": n, "device_resident_ms": statistics.median(dev_ms), "configs": []}
+cfgs = os.environ.get("CFGS", "1:0,4:0,2:1,4:1,4:2,4:3,2:3,1:0").split(",")
+for cfg in cfgs:
+    q, m = (int(x) for x in cfg.split(":"))
+    os.environ["EDV_HOST_STREAMS"] = str(q)
+    os.environ["EDV_HOST_CUMASK"] = str(m)
+    pa[:] = 0
+    call()
+    ok = bool(np.array_equal(pa, want))
+    ts = []
+    for _ in range(R):
+        t = time.perf_counter()
+        call()
+        ts.append(1e3 * (time.perf_counter() - t))
+    ts_idle = []
+    for _ in range(R):
+        time.sleep(0.005)
+        t = time.perf_counter()
+        call()
+        ts_idle.append(1e3 * (time.perf_counter() - t))
+    rec = {"streams": q, "cumask": m, "ok": ok and bool(np.array_equal(pa, want)),
+           "ms": statistics.median(ts), "ms_min": min(ts), "ms_spaced": statistics.median(ts_idle)}
+    out["configs"].append(rec)
+    print(json.dumps(rec), flush=True)
+print(json.dumps(out))
