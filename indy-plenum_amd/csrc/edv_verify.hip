@@ -163,6 +163,41 @@ struct RegBTab {
   }
 };
 
+// B entries staged through the wave's A/R LDS slice (EDV_MAIN_BREUSE): once
+// both per-lane picks of the window are done, the slice is free until the next
+// window's stage(), so issue() starts both B entries' copies into it
+// (global_load_lds, B entry 0 over the A entry, 1 over the R entry: 8 KiB of
+// each 10 KiB region) and they land during the R addition.  No registers are
+// held for them and no extra LDS is used; the B pick is an LDS read like the
+// A and R picks.
+struct ReuseBTab {
+  const int32_t* w;
+  int32_t* lds;  // the wave's A region; the R region follows at + kLdsAWords
+  int lane;
+  int j[kBTables];
+  __device__ __forceinline__ void stage(int tb, int e) { j[tb] = e; }
+  __device__ __forceinline__ void issue() {
+    // the R pick's LDS reads must be complete before the copies overwrite it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int tb = 0; tb < kBTables; tb++) {
+      const int32_t* g = w + (tb * kBEntries + j[tb]) * kBStride;
+#pragma unroll
+      for (int q = 0; q < 8; q++)
+        __builtin_amdgcn_global_load_lds(const_cast<int32_t*>(g + 4 * q), lds + tb * kLdsAWords + q * 256, 16, 0, 0);
+    }
+  }
+  __device__ __forceinline__ ge_precomp fetch(int tb) {
+    wait_staged();
+    int32_t t[32];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int4 v = reinterpret_cast<const int4*>(lds + tb * kLdsAWords + q * 256)[lane];
+      t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
+    }
+    return precomp_from_words(t);
+  }
+};
 
 // Phase 2: V8 multi-scalar walk and the identity check.  The window count is
 // the wave's maximum over its live lanes, so the loop stays wave-uniform.
@@ -206,7 +241,9 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   int32_t* wl = lds_main + (threadIdx.x >> 6) * kLdsWaveWords;
   const int lane = int(threadIdx.x & 63);
   LdsATab at{a.st.atab + j * kAWords, wl, lane}, rt{a.st.rtab + j * kAWords, wl + kLdsAWords, lane};
-#ifndef EDV_MAIN_BLDS
+#if defined(EDV_MAIN_BREUSE)
+  ReuseBTab bt{a.btab, wl, lane, {0, 0}};
+#elif !defined(EDV_MAIN_BLDS)
   RegBTab bt{a.btab, {0, 0}, {}};
 #else
   LdsBTab bt{a.btab, wl + 2 * kLdsAWords, lane};
@@ -442,6 +479,11 @@ struct DevCtx {
   hipStream_t hs[kQ] = {};
   hipEvent_t hs_staged[kQ] = {};   // pinned slot q may be refilled once its H2D copies are done
   hipEvent_t hs_end[kQ] = {};
+  // CU-masked host-path streams: sub-batch stream q confined to its own share of
+  // the CUs (EDV_HOST_CUMASK, see host_streams); hsm_key = the layout they have
+  hipStream_t hsm[kQ] = {};
+  int hsm_key = -1;
+  int ncu = 0;
   // split-prep host path (run_shard_split): copies on hcp, part q's prep on hs[q]
   hipStream_t hcp = nullptr;
   hipEvent_t part_copied[kQ] = {}, part_prepped[kQ] = {};
@@ -517,6 +559,7 @@ int ctx_init(DevCtx& c) {
   hipDeviceProp_t prop;
   HIPOK(hipGetDeviceProperties(&prop, c.phys), "hipGetDeviceProperties");
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return set_err(EDV_E_NODEV, "device is not gfx950");
+  c.ncu = prop.multiProcessorCount;
   if (!c.stream) HIPOK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking), "hipStreamCreate");
   for (int q = 0; q < kQ; q++) {
     if (!c.hs[q]) HIPOK(hipStreamCreateWithFlags(&c.hs[q], hipStreamNonBlocking), "hipStreamCreate");
@@ -730,6 +773,8 @@ int drain(DevCtx& c) {
   HIPOK(hipStreamSynchronize(c.stream), "stream sync");
   HIPOK(hipEventSynchronize(c.st_done), "scratch sync");
   for (int q = 0; q < kQ; q++) HIPOK(hipStreamSynchronize(c.hs[q]), "stream sync");
+  for (int q = 0; q < kQ; q++)
+    if (c.hsm[q]) HIPOK(hipStreamSynchronize(c.hsm[q]), "stream sync");
   if (c.hcp) HIPOK(hipStreamSynchronize(c.hcp), "stream sync");
   if (c.hac) HIPOK(hipStreamSynchronize(c.hac), "stream sync");  // async batches stay pending until edv_wait_async
   for (auto& s : c.as)
@@ -892,6 +937,39 @@ int run_shard_split(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const ui
   return 0;
 }
 
+// The Q host-path streams of run_shard.  mode 0: the plain streams hs[].  mode
+// 1..3: streams created with a CU mask (hipExtStreamCreateWithCUMask), stream q
+// owning a disjoint 1/Q of the CUs, so Q sub-batches run side by side without
+// their workgroups landing on the same CUs: 1 = contiguous CU-index ranges, 2 =
+// CU index mod Q, 3 = CU index mod 8 grouped in Q ranges (whole XCDs if the
+// mask's CU bits interleave over the 8 XCDs).
+int host_streams(DevCtx& c, int Q, int mode, hipStream_t** out) {
+  *out = c.hs;
+  if (mode <= 0 || Q <= 1) return 0;
+  const int key = mode * 16 + Q;
+  if (c.hsm_key != key) {
+    for (int q = 0; q < kQ; q++)
+      if (c.hsm[q]) {
+        HIPOK(hipStreamSynchronize(c.hsm[q]), "stream sync");
+        HIPOK(hipStreamDestroy(c.hsm[q]), "stream destroy");
+        c.hsm[q] = nullptr;
+      }
+    const int ncu = c.ncu > 0 ? c.ncu : 256;
+    const uint32_t words = uint32_t((ncu + 31) / 32);
+    for (int q = 0; q < Q; q++) {
+      std::vector<uint32_t> m(words, 0);
+      for (int i = 0; i < ncu; i++) {
+        const int owner = mode == 1 ? i * Q / ncu : (mode == 2 ? i % Q : (i % 8) * Q / 8);
+        if (owner == q) m[size_t(i / 32)] |= 1u << (i % 32);
+      }
+      HIPOK(hipExtStreamCreateWithCUMask(&c.hsm[q], words, m.data()), "hipExtStreamCreateWithCUMask");
+    }
+    c.hsm_key = key;
+  }
+  *out = c.hsm;
+  return 0;
+}
+
 // One shard on one device, host buffers: sub-batches of P requests go round
 // robin over the kQ host-path streams; per sub-batch: H2D copies (straight
 // from the caller's memory when it is pinned, else through this stream's
@@ -945,10 +1023,14 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
     if (!acc_pinned) memcpy(accept + lo, h_acc, n);
     return 0;
   }
-  for (int q = 0; q < Q; q++) HIPOK(hipStreamWaitEvent(c.hs[q], c.st_done, 0), "wait scratch");
+  int cumask = 0;
+  if (const char* e = getenv("EDV_HOST_CUMASK")) cumask = atoi(e);
+  hipStream_t* hs;
+  if ((err = host_streams(c, Q, cumask, &hs))) return err;
+  for (int q = 0; q < Q; q++) HIPOK(hipStreamWaitEvent(hs[q], c.st_done, 0), "wait scratch");
   for (uint64_t k = 0; k < nsub; k++) {
     const int q = int(k % Q);
-    hipStream_t s = c.hs[q];
+    hipStream_t s = hs[q];
     const uint64_t a = lo + k * P, b = (a + P) < hi ? (a + P) : hi, cnt = b - a;
     const uint64_t mA = off[a], mB = off[b];
     // sub-batch k's offsets live at d_off + (a - lo) + k: one private n+1 window each
@@ -999,7 +1081,7 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
   }
   // join the sub-batch streams into the library stream: the scratch's next user waits for all of them
   for (int q = 0; q < Q; q++) {
-    HIPOK(hipEventRecord(c.hs_end[q], c.hs[q]), "record");
+    HIPOK(hipEventRecord(c.hs_end[q], hs[q]), "record");
     HIPOK(hipStreamWaitEvent(c.stream, c.hs_end[q], 0), "wait");
   }
   HIPOK(hipEventRecord(c.st_done, c.stream), "record scratch");
