@@ -13,8 +13,12 @@ EDV_LIB=$R/indy-plenum_amd/variants/libedv_breuse.so EDV_PARITY_QUICK=1 timeout 
   tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread > $O/parity_breuse.log 2>&1 \
   || fail parity_breuse $O/parity_breuse.log
 tail -2 $O/parity_breuse.log
-timeout -k 10 400 python3 tools/ab_bench.py indy-plenum_amd/libedv.so indy-plenum_amd/variants/libedv_breuse.so \
-  indy-plenum_amd/libedv.so indy-plenum_amd/variants/libedv_breuse.so > $O/ab_breuse.jsonl 2> $O/ab.err \
+timeout -k 10 500 python3 tools/ab_bench.py indy-plenum_amd/libedv.so indy-plenum_amd/variants/libedv_breuse.so indy-plenum_amd/variants/libedv_breuse_early.so \
+  indy-plenum_amd/libedv.so indy-plenum_amd/variants/libedv_breuse.so indy-plenum_amd/variants/libedv_breuse_early.so > $O/ab_breuse.jsonl 2> $O/ab.err \
   || fail ab $O/ab.err
 cat $O/ab_breuse.jsonl
+export TMPDIR=/tmp
+CFGS=1:0,4:0,4:1,4:3 R=5 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $O/trace -o run \
+  --output-format csv -- python3 tools/e2e_cumask.py > $O/trace.log 2>&1 || fail trace $O/trace.log
+find $O/trace -name "*.csv" | head
 echo "session done"
