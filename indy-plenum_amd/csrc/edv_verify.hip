@@ -798,6 +798,19 @@ bool is_pinned(const void* p) {
   return attr.type == hipMemoryTypeHost;
 }
 
+// The device-side address of pinned host memory p (its mapping in the GPU's
+// address space), or null if p is not device-accessible host memory.
+const uint8_t* device_view(const void* p) {
+  if (!p) return nullptr;
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (attr.type != hipMemoryTypeHost || !attr.devicePointer) return nullptr;
+  return static_cast<const uint8_t*>(attr.devicePointer);
+}
+
 struct Seg {
   uint8_t* dst;
   const uint8_t* src;
@@ -970,6 +983,38 @@ int host_streams(DevCtx& c, int Q, int mode, hipStream_t** out) {
   return 0;
 }
 
+// Zero-copy form of run_shard for pinned inputs (EDV_ZERO_COPY=1, measurement
+// A/B): the prep kernel reads sigs, pks, offsets and message bytes from the
+// caller's pinned host memory over the link while it computes (no H2D copy
+// before it), and the main kernel writes the verdicts straight into the
+// caller's pinned accept bytes.  Used only when every pointer has a device view,
+// sigs/pks are 16-byte aligned, there are message bytes, and the 16 bytes the
+// message loads may read past the last message (edv_verify_core.h
+// msg_words_tail) lie in the same 4 KiB page as its last byte, so the kernels
+// touch no page the caller did not pin.  1 = not applicable (caller copies).
+int run_shard_zero_copy(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                        const uint64_t* off, uint64_t lo, uint64_t hi, uint8_t* accept, bool varied) {
+  const uint64_t n = hi - lo, mbase = off[lo], mend = off[hi];
+  if (mend == mbase) return 1;
+  const uintptr_t e = reinterpret_cast<uintptr_t>(msgs + mend);
+  if (((e + 15) >> 12) != ((e - 1) >> 12)) return 1;
+  const uint8_t* ds = device_view(sigs + 64 * lo);
+  const uint8_t* dp = device_view(pks + 32 * lo);
+  const uint8_t* dm = device_view(msgs + mbase);
+  const uint8_t* dof = device_view(off + lo);
+  uint8_t* da = const_cast<uint8_t*>(device_view(accept + lo));
+  if (!ds || !dp || !dm || !dof || !da) return 1;
+  if ((reinterpret_cast<uintptr_t>(ds) & 15) || (reinterpret_cast<uintptr_t>(dp) & 15) ||
+      (reinterpret_cast<uintptr_t>(dof) & 7))
+    return 1;
+  int err;
+  if ((err = launch(c, ds, dp, dm, reinterpret_cast<const uint64_t*>(dof), mbase, n, da, c.stream,
+                    varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH)))
+    return err;
+  HIPOK(hipStreamSynchronize(c.stream), "stream sync");
+  return 0;
+}
+
 // One shard on one device, host buffers: sub-batches of P requests go round
 // robin over the kQ host-path streams; per sub-batch: H2D copies (straight
 // from the caller's memory when it is pinned, else through this stream's
@@ -1005,6 +1050,10 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
   if (!acc_pinned && c.acc_host.ensure(n)) return EDV_E_OOM;
   // bucket by SHA block count only when the shard's messages differ in block count
   const bool varied = !scan_offsets(off, lo, hi).uniform;
+  if (pinned && acc_pinned && getenv("EDV_ZERO_COPY")) {
+    const int zc = run_shard_zero_copy(c, sigs, pks, msgs, off, lo, hi, accept, varied);
+    if (zc <= 0) return zc;
+  }
   const uint32_t flags = varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH;
   uint8_t* d_sigs = static_cast<uint8_t*>(c.sigs.p);
   uint8_t* d_pks = static_cast<uint8_t*>(c.pks.p);

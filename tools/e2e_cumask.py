@@ -1,7 +1,8 @@
 """Synchronous edv_verify_batch on pinned host buffers at C2 (65,536 x 256 B):
 one sub-batch (the default) against Q sub-batches on Q streams, plain or each
 confined to its own 1/Q of the CUs (EDV_HOST_CUMASK modes 1-3, see
-host_streams in csrc/edv_verify.hip).  Median of R calls back to back, and of
+host_streams in csrc/edv_verify.hip), and the zero-copy form (cfg suffix :z,
+EDV_ZERO_COPY: the kernels read the pinned inputs over the link, no H2D copy).  Median of R calls back to back, and of
 R calls 5 ms apart (the GPU idles in between, as a Node's calls would).
 Verdicts checked on every configuration.  Measurement only."""
 import json
@@ -47,11 +48,17 @@ for _ in range(R):
     edv.sync(0)
     dev_ms.append(1e3 * (time.perf_counter() - t))
 out = {"n": n, "device_resident_ms": statistics.median(dev_ms), "configs": []}
-cfgs = os.environ.get("CFGS", "1:0,4:0,2:1,4:1,4:2,4:3,2:3,1:0").split(",")
+cfgs = os.environ.get("CFGS", "1:0,1:0:z,4:0,2:1,4:1,4:2,4:3,2:3,1:0,1:0:z").split(",")
 for cfg in cfgs:
-    q, m = (int(x) for x in cfg.split(":"))
+    parts = cfg.split(":")
+    q, m = int(parts[0]), int(parts[1])
+    zc = len(parts) > 2 and parts[2] == "z"
     os.environ["EDV_HOST_STREAMS"] = str(q)
     os.environ["EDV_HOST_CUMASK"] = str(m)
+    if zc:
+        os.environ["EDV_ZERO_COPY"] = "1"
+    else:
+        os.environ.pop("EDV_ZERO_COPY", None)
     pa[:] = 0
     call()
     ok = bool(np.array_equal(pa, want))
@@ -66,7 +73,7 @@ for cfg in cfgs:
         t = time.perf_counter()
         call()
         ts_idle.append(1e3 * (time.perf_counter() - t))
-    rec = {"streams": q, "cumask": m, "ok": ok and bool(np.array_equal(pa, want)),
+    rec = {"streams": q, "cumask": m, "zero_copy": zc, "ok": ok and bool(np.array_equal(pa, want)),
            "ms": statistics.median(ts), "ms_min": min(ts), "ms_spaced": statistics.median(ts_idle)}
     out["configs"].append(rec)
     print(json.dumps(rec), flush=True)

@@ -18,7 +18,9 @@ timeout -k 10 500 python3 tools/ab_bench.py indy-plenum_amd/libedv.so indy-plenu
   || fail ab $O/ab.err
 cat $O/ab_breuse.jsonl
 export TMPDIR=/tmp
-CFGS=1:0,4:0,4:1,4:3 R=5 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $O/trace -o run \
+CFGS=1:0,4:0,4:1,1:0:z R=5 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $O/trace -o run \
   --output-format csv -- python3 tools/e2e_cumask.py > $O/trace.log 2>&1 || fail trace $O/trace.log
 find $O/trace -name "*.csv" | head
+python3 tools/trace_overlap.py $O/trace 1:0,4:0,4:1,1:0:z 5 > $O/trace_overlap.json || true
+cat $O/trace_overlap.json
 echo "session done"
