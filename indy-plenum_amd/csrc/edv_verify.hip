@@ -479,11 +479,6 @@ struct DevCtx {
   hipStream_t hs[kQ] = {};
   hipEvent_t hs_staged[kQ] = {};   // pinned slot q may be refilled once its H2D copies are done
   hipEvent_t hs_end[kQ] = {};
-  // CU-masked host-path streams: sub-batch stream q confined to its own share of
-  // the CUs (EDV_HOST_CUMASK, see host_streams); hsm_key = the layout they have
-  hipStream_t hsm[kQ] = {};
-  int hsm_key = -1;
-  int ncu = 0;
   // split-prep host path (run_shard_split): copies on hcp, part q's prep on hs[q]
   hipStream_t hcp = nullptr;
   hipEvent_t part_copied[kQ] = {}, part_prepped[kQ] = {};
@@ -559,7 +554,6 @@ int ctx_init(DevCtx& c) {
   hipDeviceProp_t prop;
   HIPOK(hipGetDeviceProperties(&prop, c.phys), "hipGetDeviceProperties");
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return set_err(EDV_E_NODEV, "device is not gfx950");
-  c.ncu = prop.multiProcessorCount;
   if (!c.stream) HIPOK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking), "hipStreamCreate");
   for (int q = 0; q < kQ; q++) {
     if (!c.hs[q]) HIPOK(hipStreamCreateWithFlags(&c.hs[q], hipStreamNonBlocking), "hipStreamCreate");
@@ -773,8 +767,6 @@ int drain(DevCtx& c) {
   HIPOK(hipStreamSynchronize(c.stream), "stream sync");
   HIPOK(hipEventSynchronize(c.st_done), "scratch sync");
   for (int q = 0; q < kQ; q++) HIPOK(hipStreamSynchronize(c.hs[q]), "stream sync");
-  for (int q = 0; q < kQ; q++)
-    if (c.hsm[q]) HIPOK(hipStreamSynchronize(c.hsm[q]), "stream sync");
   if (c.hcp) HIPOK(hipStreamSynchronize(c.hcp), "stream sync");
   if (c.hac) HIPOK(hipStreamSynchronize(c.hac), "stream sync");  // async batches stay pending until edv_wait_async
   for (auto& s : c.as)
@@ -796,19 +788,6 @@ bool is_pinned(const void* p) {
     return false;
   }
   return attr.type == hipMemoryTypeHost;
-}
-
-// The device-side address of pinned host memory p (its mapping in the GPU's
-// address space), or null if p is not device-accessible host memory.
-const uint8_t* device_view(const void* p) {
-  if (!p) return nullptr;
-  hipPointerAttribute_t attr;
-  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  if (attr.type != hipMemoryTypeHost || !attr.devicePointer) return nullptr;
-  return static_cast<const uint8_t*>(attr.devicePointer);
 }
 
 struct Seg {
@@ -950,71 +929,6 @@ int run_shard_split(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const ui
   return 0;
 }
 
-// The Q host-path streams of run_shard.  mode 0: the plain streams hs[].  mode
-// 1..3: streams created with a CU mask (hipExtStreamCreateWithCUMask), stream q
-// owning a disjoint 1/Q of the CUs, so Q sub-batches run side by side without
-// their workgroups landing on the same CUs: 1 = contiguous CU-index ranges, 2 =
-// CU index mod Q, 3 = CU index mod 8 grouped in Q ranges (whole XCDs if the
-// mask's CU bits interleave over the 8 XCDs).
-int host_streams(DevCtx& c, int Q, int mode, hipStream_t** out) {
-  *out = c.hs;
-  if (mode <= 0 || Q <= 1) return 0;
-  const int key = mode * 16 + Q;
-  if (c.hsm_key != key) {
-    for (int q = 0; q < kQ; q++)
-      if (c.hsm[q]) {
-        HIPOK(hipStreamSynchronize(c.hsm[q]), "stream sync");
-        HIPOK(hipStreamDestroy(c.hsm[q]), "stream destroy");
-        c.hsm[q] = nullptr;
-      }
-    const int ncu = c.ncu > 0 ? c.ncu : 256;
-    const uint32_t words = uint32_t((ncu + 31) / 32);
-    for (int q = 0; q < Q; q++) {
-      std::vector<uint32_t> m(words, 0);
-      for (int i = 0; i < ncu; i++) {
-        const int owner = mode == 1 ? i * Q / ncu : (mode == 2 ? i % Q : (i % 8) * Q / 8);
-        if (owner == q) m[size_t(i / 32)] |= 1u << (i % 32);
-      }
-      HIPOK(hipExtStreamCreateWithCUMask(&c.hsm[q], words, m.data()), "hipExtStreamCreateWithCUMask");
-    }
-    c.hsm_key = key;
-  }
-  *out = c.hsm;
-  return 0;
-}
-
-// Zero-copy form of run_shard for pinned inputs (EDV_ZERO_COPY=1, measurement
-// A/B): the prep kernel reads sigs, pks, offsets and message bytes from the
-// caller's pinned host memory over the link while it computes (no H2D copy
-// before it), and the main kernel writes the verdicts straight into the
-// caller's pinned accept bytes.  Used only when every pointer has a device view,
-// sigs/pks are 16-byte aligned, there are message bytes, and the 16 bytes the
-// message loads may read past the last message (edv_verify_core.h
-// msg_words_tail) lie in the same 4 KiB page as its last byte, so the kernels
-// touch no page the caller did not pin.  1 = not applicable (caller copies).
-int run_shard_zero_copy(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
-                        const uint64_t* off, uint64_t lo, uint64_t hi, uint8_t* accept, bool varied) {
-  const uint64_t n = hi - lo, mbase = off[lo], mend = off[hi];
-  if (mend == mbase) return 1;
-  const uintptr_t e = reinterpret_cast<uintptr_t>(msgs + mend);
-  if (((e + 15) >> 12) != ((e - 1) >> 12)) return 1;
-  const uint8_t* ds = device_view(sigs + 64 * lo);
-  const uint8_t* dp = device_view(pks + 32 * lo);
-  const uint8_t* dm = device_view(msgs + mbase);
-  const uint8_t* dof = device_view(off + lo);
-  uint8_t* da = const_cast<uint8_t*>(device_view(accept + lo));
-  if (!ds || !dp || !dm || !dof || !da) return 1;
-  if ((reinterpret_cast<uintptr_t>(ds) & 15) || (reinterpret_cast<uintptr_t>(dp) & 15) ||
-      (reinterpret_cast<uintptr_t>(dof) & 7))
-    return 1;
-  int err;
-  if ((err = launch(c, ds, dp, dm, reinterpret_cast<const uint64_t*>(dof), mbase, n, da, c.stream,
-                    varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH)))
-    return err;
-  HIPOK(hipStreamSynchronize(c.stream), "stream sync");
-  return 0;
-}
-
 // One shard on one device, host buffers: sub-batches of P requests go round
 // robin over the kQ host-path streams; per sub-batch: H2D copies (straight
 // from the caller's memory when it is pinned, else through this stream's
@@ -1050,10 +964,6 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
   if (!acc_pinned && c.acc_host.ensure(n)) return EDV_E_OOM;
   // bucket by SHA block count only when the shard's messages differ in block count
   const bool varied = !scan_offsets(off, lo, hi).uniform;
-  if (pinned && acc_pinned && getenv("EDV_ZERO_COPY")) {
-    const int zc = run_shard_zero_copy(c, sigs, pks, msgs, off, lo, hi, accept, varied);
-    if (zc <= 0) return zc;
-  }
   const uint32_t flags = varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH;
   uint8_t* d_sigs = static_cast<uint8_t*>(c.sigs.p);
   uint8_t* d_pks = static_cast<uint8_t*>(c.pks.p);
@@ -1072,10 +982,7 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
     if (!acc_pinned) memcpy(accept + lo, h_acc, n);
     return 0;
   }
-  int cumask = 0;
-  if (const char* e = getenv("EDV_HOST_CUMASK")) cumask = atoi(e);
-  hipStream_t* hs;
-  if ((err = host_streams(c, Q, cumask, &hs))) return err;
+  hipStream_t* hs = c.hs;
   for (int q = 0; q < Q; q++) HIPOK(hipStreamWaitEvent(hs[q], c.st_done, 0), "wait scratch");
   for (uint64_t k = 0; k < nsub; k++) {
     const int q = int(k % Q);
@@ -1220,6 +1127,7 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
   s.acc_pinned = is_pinned(accept);
   if (!s.acc_pinned && s.acc_host.ensure(n)) return EDV_E_OOM;
   const bool varied = !scan_offsets(off, 0, n).uniform;
+  const uint32_t lflags = varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH;
   const uint8_t *src_s = sigs, *src_p = pks, *src_m = msgs + mbase;
   const uint8_t* src_o = reinterpret_cast<const uint8_t*>(off);
   if (!pinned) {
@@ -1242,7 +1150,6 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
     HIPOK(hipEventRecord(s.copied, c.hcp), "record");
     HIPOK(hipStreamWaitEvent(c.hac, s.copied, 0), "wait copy");
   }
-  const uint32_t lflags = varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH;
   if ((err = own ? launch_own(c, s.cb, kSmallAsync, d_sigs, d_pks, d_msgs, d_off, mbase, n, d_acc, ks, lflags)
                  : launch(c, d_sigs, d_pks, d_msgs, d_off, mbase, n, d_acc, ks, lflags)))
     return err;

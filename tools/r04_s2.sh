@@ -7,6 +7,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/r04/s2; mkdir -p $O; cd $R
 fail() { echo "FAILED: $1"; tail -30 "$2"; exit 1; }
 timeout -k 10 240 python3 tools/latency_vs_n.py > $O/latency_vs_n.jsonl 2> $O/lat.err || fail lat $O/lat.err
 cat $O/latency_vs_n.jsonl
+timeout -k 10 240 python3 tools/small_batch_latency.py > $O/small_batch_latency.jsonl 2> $O/sbl.err || fail sbl $O/sbl.err
+cat $O/small_batch_latency.jsonl
 timeout -k 10 300 python3 tools/e2e_cumask.py > $O/e2e_cumask.jsonl 2> $O/cumask.err || fail cumask $O/cumask.err
 tail -1 $O/e2e_cumask.jsonl
 EDV_LIB=$R/indy-plenum_amd/variants/libedv_breuse.so EDV_PARITY_QUICK=1 timeout -k 10 400 python3 -u -m pytest \
