@@ -163,42 +163,6 @@ struct RegBTab {
   }
 };
 
-// B entries staged through the wave's A/R LDS slice (EDV_MAIN_BREUSE): once
-// both per-lane picks of the window are done, the slice is free until the next
-// window's stage(), so issue() starts both B entries' copies into it
-// (global_load_lds, B entry 0 over the A entry, 1 over the R entry: 8 KiB of
-// each 10 KiB region) and they land during the R addition.  No registers are
-// held for them and no extra LDS is used; the B pick is an LDS read like the
-// A and R picks.
-struct ReuseBTab {
-  const int32_t* w;
-  int32_t* lds;  // the wave's A region; the R region follows at + kLdsAWords
-  int lane;
-  int j[kBTables];
-  __device__ __forceinline__ void stage(int tb, int e) { j[tb] = e; }
-  __device__ __forceinline__ void issue() {
-    // the R pick's LDS reads must be complete before the copies overwrite it
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int tb = 0; tb < kBTables; tb++) {
-      const int32_t* g = w + (tb * kBEntries + j[tb]) * kBStride;
-#pragma unroll
-      for (int q = 0; q < 8; q++)
-        __builtin_amdgcn_global_load_lds(const_cast<int32_t*>(g + 4 * q), lds + tb * kLdsAWords + q * 256, 16, 0, 0);
-    }
-  }
-  __device__ __forceinline__ ge_precomp fetch(int tb) {
-    wait_staged();
-    int32_t t[32];
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int4 v = reinterpret_cast<const int4*>(lds + tb * kLdsAWords + q * 256)[lane];
-      t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
-    }
-    return precomp_from_words(t);
-  }
-};
-
 // Phase 2: V8 multi-scalar walk and the identity check.  The window count is
 // the wave's maximum over its live lanes, so the loop stays wave-uniform.
 __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
@@ -241,9 +205,7 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   int32_t* wl = lds_main + (threadIdx.x >> 6) * kLdsWaveWords;
   const int lane = int(threadIdx.x & 63);
   LdsATab at{a.st.atab + j * kAWords, wl, lane}, rt{a.st.rtab + j * kAWords, wl + kLdsAWords, lane};
-#if defined(EDV_MAIN_BREUSE)
-  ReuseBTab bt{a.btab, wl, lane, {0, 0}};
-#elif !defined(EDV_MAIN_BLDS)
+#ifndef EDV_MAIN_BLDS
   RegBTab bt{a.btab, {0, 0}, {}};
 #else
   LdsBTab bt{a.btab, wl + 2 * kLdsAWords, lane};

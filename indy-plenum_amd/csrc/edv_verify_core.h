@@ -778,7 +778,6 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
     const bool sw = w == nwin - 6, sb = w == 8;
     if (sw) EDV_STAMP(5);
     ge_p3 p3;
-#ifndef EDV_EARLY_APICK
     if (w == nwin - 1) {
       p3 = ge_p3_identity();
     } else {
@@ -789,20 +788,6 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
     if (sw) EDV_STAMP(6);
     if (sb) EDV_STAMP(11);
     const ge_cached ea = at.fetch();
-#else
-    // A/B variant: the A entry's LDS pick before the window's last doubling
-    ge_cached ea;
-    if (w == nwin - 1) {
-      p3 = ge_p3_identity();
-      ea = at.fetch();
-    } else {
-#pragma unroll 1
-      for (int d = 0; d < kAWin - 2; d++) acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
-      ge_p1p1 last = ge_p2_dbl(ge_p1p1_to_p2(ge_p2_dbl(acc)));
-      ea = at.fetch();
-      p3 = ge_p1p1_to_p3(last);
-    }
-#endif
     if (sw) EDV_STAMP(7);
     p3 = ge_p1p1_to_p3(ge_add(p3, ge_cached_cneg(ea, dA < 0)));
     if (sw) EDV_STAMP(8);
