@@ -693,6 +693,9 @@ def parse_args():
     ap.add_argument("--spawn", action="store_true", help="launch the ranks from this process even for one GPU")
     ap.add_argument("--pipeline", action="store_true",
                     help="time the two-stream pipelined submission (prep of step k+1 beside main of step k)")
+    ap.add_argument("--split-prep", action="store_true",
+                    help="with --pipeline: only the hash side of step k+1 beside main of step k, the point sides "
+                         "after it (EDV_FLAG_SPLIT_PREP)")
     return ap.parse_args()
 
 
@@ -725,9 +728,11 @@ def main():
 
     s = edv.stream(dev)
 
+    split = edv.FLAG_SPLIT_PREP if args.split_prep else 0
+
     def step():
         if args.pipeline:
-            batch.submit()
+            batch.submit(split)
         else:
             batch.verify(stream=s)
 
@@ -841,7 +846,9 @@ def main():
         "roofline": roofline,
         "verdicts_as_expected": verdicts_ok,
         **({"multi_gpu": out_multi} if world > 1 else {}),
-        "timing": {"mode": "pipelined (prep of step k+1 beside main of step k)" if args.pipeline else "sequential",
+        "timing": {"mode": ("pipelined, split prep (hash side of step k+1 beside main of step k, point sides after "
+                            "it)" if args.split_prep else "pipelined (prep of step k+1 beside main of step k)")
+                           if args.pipeline else "sequential",
                    "reps_s": reps, "median_of": len(reps), "warmup_steps_run": warm_steps,
                    "kernel_sum_ms": path_ms, "gap_ms_per_step": ms_step - path_ms * n / pn,
                    "launch": "ranks started by bench.py" if os.environ.get("EDV_BENCH_TOKEN") else

@@ -118,6 +118,8 @@ int edv_verify_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uint
  * device mode of edv_set_length_buckets for this call only). */
 #define EDV_FLAG_UNIFORM_LENGTH 1u /* every message has the same SHA-512 block count: no buckets */
 #define EDV_FLAG_BUCKETS 2u        /* always bucket by block count */
+#define EDV_FLAG_SPLIT_PREP 4u     /* edv_verify_batch_dev_pipelined only: the hash side of batch k+1's
+                                      prep runs beside batch k's main kernel, the point sides after it */
 int edv_verify_batch_dev_flags(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
                                const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept,
                                int device, void *stream, uint32_t flags);

@@ -49,6 +49,10 @@ struct VerifyArgs {
   uint8_t* accept;        // indexed by global signature index
   ChunkState st;
   const int32_t* btab;    // kBTables x kBEntries x kBStride
+  // prep sides this launch runs: workgroup b runs side side0 + b % nsides
+  // (0 hash, 1 A, 2 R); 0 / 3 = all three, 0 / 1 = the hash side, 1 / 2 = the points
+  int32_t side0;
+  int32_t nsides;
 };
 
 // Per-signature A table in HBM, signature-major: signature i's 360 words are

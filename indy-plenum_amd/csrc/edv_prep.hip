@@ -30,7 +30,8 @@ namespace edv {
 namespace {
 
 // Phase 1 in three independent sides, interleaved by workgroup (block b runs
-// side b % 3 of slots [(b / 3) 256, +256)): 0 = V2-V4 checks, V6/V7 hash,
+// side side0 + b % nsides of slots [(b / nsides) 256, +256); all three by default,
+// the split pipeline launches the hash side and the two point sides apart): 0 = V2-V4 checks, V6/V7 hash,
 // half-size scalars and digits; 1 = decompress A, 0..8 x (-A) table; 2 = the
 // same for R.  They share no data, so they run side by side (three waves per
 // SIMD at 64k signatures where one kernel per side would leave one wave each
@@ -54,8 +55,9 @@ __device__ __forceinline__ void prep_point_side(const VerifyArgs& a, uint64_t j,
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EDV_PREP_WAVES, 8))) void edv_prep_kernel(
     VerifyArgs a) {
   EDV_STAMP(0);
-  const int side = int(blockIdx.x % 3);
-  const uint64_t j = uint64_t(blockIdx.x / 3) * kBlock + threadIdx.x;  // slot within the chunk
+  const uint32_t ns = uint32_t(a.nsides);
+  const int side = a.side0 + int(blockIdx.x % ns);
+  const uint64_t j = uint64_t(blockIdx.x / ns) * kBlock + threadIdx.x;  // slot within the chunk
 #ifdef EDV_AB_SIDES  // measurement-only variant (wrong verdicts): bit k set = run side k
   if (!((EDV_AB_SIDES >> side) & 1)) return;
 #endif

@@ -476,6 +476,7 @@ struct DevCtx {
   ChunkBufs pst[2];
   hipStream_t sp = nullptr, sm = nullptr;
   hipEvent_t prep_done[2] = {nullptr, nullptr}, main_done[2] = {nullptr, nullptr}, inputs_ready = nullptr;
+  hipEvent_t perm_done[2] = {nullptr, nullptr};  // split prep: state set b's bucket permutation is written
   bool pending[2] = {false, false};
   int next = 0;
 };
@@ -596,24 +597,38 @@ VerifyArgs make_args(const DevCtx& c, ChunkBufs& b, const uint8_t* d_sigs, const
   va.btab = c.btab;
   va.base = 0;
   va.n = 0;
+  va.side0 = 0;
+  va.nsides = 3;
   return va;
 }
 
-// [length buckets,] prep kernel of one chunk on stream s (ctr: this stream's histogram + cursors)
-int launch_prep(uint32_t* ctr, const VerifyArgs& va, const uint64_t* d_off, bool bucket, hipStream_t s) {
+// length buckets of one chunk on stream s (ctr: this stream's histogram + cursors)
+int launch_buckets(uint32_t* ctr, const VerifyArgs& va, const uint64_t* d_off, hipStream_t s) {
+  const unsigned blocks = unsigned((va.n + kBlock - 1) / kBlock);
+  HIPOK(hipMemsetAsync(ctr, 0, 2 * kBuckets * 4, s), "memset buckets");
+  edv_bucket_hist_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, va.base, va.n, ctr);
+  edv_bucket_scatter_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, va.base, va.n, ctr, ctr + kBuckets,
+                                                                   const_cast<uint32_t*>(va.st.perm));
+  HIPOK(hipGetLastError(), "bucket launch");
+  return 0;
+}
+// the prep kernel over the sides va.side0 .. va.side0 + va.nsides - 1
+int launch_prep_sides(const VerifyArgs& va, hipStream_t s) {
 #ifdef EDV_MEASURE_NO_VERIFY
   return 0;  // measurement build: see launch_main
 #endif
   const unsigned blocks = unsigned((va.n + kBlock - 1) / kBlock);
-  if (bucket) {
-    HIPOK(hipMemsetAsync(ctr, 0, 2 * kBuckets * 4, s), "memset buckets");
-    edv_bucket_hist_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, va.base, va.n, ctr);
-    edv_bucket_scatter_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(d_off, va.base, va.n, ctr, ctr + kBuckets,
-                                                                     const_cast<uint32_t*>(va.st.perm));
-    HIPOK(hipGetLastError(), "bucket launch");
-  }
-  HIPOK(launch_prep_kernel(3 * blocks, s, va), "prep launch");  // hash, A and R sides
+  HIPOK(launch_prep_kernel(unsigned(va.nsides) * blocks, s, va), "prep launch");
   return 0;
+}
+// [length buckets,] prep kernel (all three sides) of one chunk on stream s
+int launch_prep(uint32_t* ctr, const VerifyArgs& va, const uint64_t* d_off, bool bucket, hipStream_t s) {
+#ifdef EDV_MEASURE_NO_VERIFY
+  return 0;  // measurement build: see launch_main
+#endif
+  int err;
+  if (bucket && (err = launch_buckets(ctr, va, d_off, s))) return err;
+  return launch_prep_sides(va, s);  // hash, A and R sides
 }
 int launch_main(const VerifyArgs& va, hipStream_t s) {
 #ifdef EDV_MEASURE_NO_VERIFY
@@ -689,6 +704,7 @@ int pipe_init(DevCtx& c) {
   for (int b = 0; b < 2; b++) {
     if (!c.prep_done[b]) HIPOK(hipEventCreateWithFlags(&c.prep_done[b], hipEventDisableTiming), "event");
     if (!c.main_done[b]) HIPOK(hipEventCreateWithFlags(&c.main_done[b], hipEventDisableTiming), "event");
+    if (!c.perm_done[b]) HIPOK(hipEventCreateWithFlags(&c.perm_done[b], hipEventDisableTiming), "event");
   }
   if (!c.inputs_ready) HIPOK(hipEventCreateWithFlags(&c.inputs_ready, hipEventDisableTiming), "event");
   c.pipe_ready = true;
@@ -704,8 +720,10 @@ int launch_pipelined(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, con
   int err;
   if ((err = pipe_init(c))) return err;
   const bool bucket = bucketing_enabled(c, flags);
+  const bool split = (flags & EDV_FLAG_SPLIT_PREP) != 0;
   HIPOK(hipEventRecord(c.inputs_ready, c.stream), "record");
   HIPOK(hipStreamWaitEvent(c.sp, c.inputs_ready, 0), "wait");
+  if (split) HIPOK(hipStreamWaitEvent(c.sm, c.inputs_ready, 0), "wait");
   for (uint64_t base = 0; base < n; base += c.chunk) {
     const int b = c.next;
     c.next ^= 1;
@@ -714,6 +732,32 @@ int launch_pipelined(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, con
     va.base = base;
     va.n = (n - base) < c.chunk ? (n - base) : c.chunk;
     if (c.pending[b]) HIPOK(hipStreamWaitEvent(c.sp, c.main_done[b], 0), "wait");
+    if (split) {
+      // Split prep: the hash side (one latency-bound SHA-512 chain per lane,
+      // light on issue) goes on sp, where it runs beside the main kernel of the
+      // previous chunk; the two point sides (issue-bound exponentiations) go on
+      // sm in front of this chunk's main kernel, which waits for the hash side.
+      // State set b's previous main kernel ran on sm, so sm needs no wait for
+      // it; sp waited for it above.
+      if (bucket) {
+        if ((err = launch_buckets(bucket_ctr(cb, 0), va, d_off, c.sp))) return err;
+        HIPOK(hipEventRecord(c.perm_done[b], c.sp), "record");
+        HIPOK(hipStreamWaitEvent(c.sm, c.perm_done[b], 0), "wait");
+      }
+      VerifyArgs vh = va, vp = va;
+      vh.side0 = 0;
+      vh.nsides = 1;
+      vp.side0 = 1;
+      vp.nsides = 2;
+      if ((err = launch_prep_sides(vh, c.sp))) return err;
+      HIPOK(hipEventRecord(c.prep_done[b], c.sp), "record");
+      if ((err = launch_prep_sides(vp, c.sm))) return err;
+      HIPOK(hipStreamWaitEvent(c.sm, c.prep_done[b], 0), "wait");
+      if ((err = launch_main(va, c.sm))) return err;
+      HIPOK(hipEventRecord(c.main_done[b], c.sm), "record");
+      c.pending[b] = true;
+      continue;
+    }
     if ((err = launch_prep(bucket_ctr(cb, 0), va, d_off, bucket, c.sp))) return err;
     HIPOK(hipEventRecord(c.prep_done[b], c.sp), "record");
     HIPOK(hipStreamWaitEvent(c.sm, c.prep_done[b], 0), "wait");

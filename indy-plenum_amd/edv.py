@@ -31,6 +31,7 @@ EDV_E_HIP = -3
 EDV_E_OOM = -4
 FLAG_UNIFORM_LENGTH = 1  # every message has the same SHA-512 block count: no length buckets
 FLAG_BUCKETS = 2         # always bucket by SHA-512 block count
+FLAG_SPLIT_PREP = 4      # pipelined path: batch k+1's hash side beside batch k's main kernel
 
 
 class EdvUnavailable(RuntimeError):

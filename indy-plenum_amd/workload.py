@@ -233,10 +233,11 @@ class DeviceBatch:
         edv.verify_device(self.d_sigs.ptr, self.d_pks.ptr, self.d_msgs.ptr, self.d_off.ptr, self.n,
                           self.d_accept.ptr, self.device, stream=stream, flags=self.flags)
 
-    def submit(self):
-        """Pipelined verify (edv_verify_batch_dev_pipelined); results after edv.pipeline_sync."""
+    def submit(self, extra_flags=0):
+        """Pipelined verify (edv_verify_batch_dev_pipelined); results after edv.pipeline_sync.
+        extra_flags: edv.FLAG_SPLIT_PREP runs the hash side beside the previous main kernel."""
         edv.verify_device_pipelined(self.d_sigs.ptr, self.d_pks.ptr, self.d_msgs.ptr, self.d_off.ptr, self.n,
-                                    self.d_accept.ptr, self.device, flags=self.flags)
+                                    self.d_accept.ptr, self.device, flags=self.flags | extra_flags)
 
     def accept(self, out=None):
         """The verdict bytes (D2H), into `out` (a host slice of n bytes) if given."""
