@@ -637,6 +637,14 @@ def c4_leg(dev, steps, reps, n=65536):
     edv.pipeline_sync(dev)
     tp = timed_steps(b.submit, lambda: edv.pipeline_sync(dev), steps, reps, rdv)
     okp = bool(np.array_equal(b.accept(), exp))
+    # the split pipeline: only the hash side (one latency-bound SHA-512 chain per lane, ~17 blocks here)
+    # of step k+1 beside main of step k, the issue-bound point sides in front of step k+1's main
+    for _ in range(3):
+        b.submit(edv.FLAG_SPLIT_PREP)
+    edv.pipeline_sync(dev)
+    b.d_accept.upload(np.full(n, 7, np.uint8))
+    ts_split = timed_steps(lambda: b.submit(edv.FLAG_SPLIT_PREP), lambda: edv.pipeline_sync(dev), steps, reps, rdv)
+    oks = bool(np.array_equal(b.accept(), exp))
     return {"workload": "C4: %d Ed25519 verifies per step, messages uniform in 200..4,096 B (mean %.0f B), "
                         "length-bucketed SHA-512, 5 %% invalid over %s" % (n, lens.mean(), ", ".join(workload.DAMAGE_KINDS)),
             "verifies_per_s": n * steps / el, "ms_per_step": 1e3 * el / steps, "reps_s": ts,
@@ -647,7 +655,12 @@ def c4_leg(dev, steps, reps, n=65536):
             "pipelined": {"verifies_per_s": n * steps / statistics.median(tp), "reps_s": tp,
                           "verdicts_as_expected": okp,
                           "what": "edv_verify_batch_dev_pipelined back to back (prep of step k+1 on a second stream "
-                                  "beside main of step k)"}}
+                                  "beside main of step k)"},
+            "pipelined_split": {"verifies_per_s": n * steps / statistics.median(ts_split), "reps_s": ts_split,
+                                "verdicts_as_expected": oks,
+                                "what": "edv_verify_batch_dev_pipelined with EDV_FLAG_SPLIT_PREP: the hash side of "
+                                        "step k+1 beside main of step k, the point sides in front of step k+1's "
+                                        "main"}}
 
 
 def c5_leg(n=20000, n_cpu=2000):

@@ -165,12 +165,7 @@ struct RegBTab {
 
 // Phase 2: V8 multi-scalar walk and the identity check.  The window count is
 // the wave's maximum over its live lanes, so the loop stays wave-uniform.
-__global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
-  __shared__ int32_t lds_main[(kBlock / 64) * kLdsWaveWords];
-#ifdef EDV_AB_SIDES  // prep-only measurement variant: the prep state is incomplete, so do nothing here
-  return;
-#endif
-  MAIN_STAMP(0);
+__device__ __forceinline__ void main_body(const VerifyArgs& a, int32_t* lds_main) {
   const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
   const bool live = j < a.n && a.st.alive[j] && a.st.alive[a.st.cap + j] && a.st.alive[2 * a.st.cap + j];
   const uint32_t* d = a.st.dig + j;
@@ -213,6 +208,29 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   MAIN_STAMP(1);
   a.accept[i] = main_one(da, db, bw, nwin, (wf >> 8) & 1, at, rt, bt) ? 1 : 0;
   MAIN_STAMP(15);
+}
+
+__global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
+  __shared__ int32_t lds_main[(kBlock / 64) * kLdsWaveWords];
+#ifdef EDV_AB_SIDES  // prep-only measurement variant: the prep state is incomplete, so do nothing here
+  return;
+#endif
+  MAIN_STAMP(0);
+  main_body(a, lds_main);
+}
+
+// The split pipeline's main kernel (EDV_FLAG_SPLIT_PREP): the same walk at a
+// raised issue priority, so the next batch's hash-side waves sharing its SIMDs
+// (latency-bound SHA-512 chains) take the cycles it leaves, instead of
+// round-robin turns; in the plain paths the raised priority only costs (C2
+// sequential 0.698 against 0.678 ms, profiles/r04/ab_prio_s8.jsonl).
+#ifndef EDV_SPLIT_MAIN_PRIO
+#define EDV_SPLIT_MAIN_PRIO 2
+#endif
+__global__ __launch_bounds__(kBlock) void edv_main_kernel_prio(VerifyArgs a) {
+  __shared__ int32_t lds_main[(kBlock / 64) * kLdsWaveWords];
+  __builtin_amdgcn_s_setprio(EDV_SPLIT_MAIN_PRIO);
+  main_body(a, lds_main);
 }
 
 // Comb rows for the batch signer, in global memory (528 KB, L2-resident).
@@ -630,7 +648,7 @@ int launch_prep(uint32_t* ctr, const VerifyArgs& va, const uint64_t* d_off, bool
   if (bucket && (err = launch_buckets(ctr, va, d_off, s))) return err;
   return launch_prep_sides(va, s);  // hash, A and R sides
 }
-int launch_main(const VerifyArgs& va, hipStream_t s) {
+int launch_main(const VerifyArgs& va, hipStream_t s, bool prio = false) {
 #ifdef EDV_MEASURE_NO_VERIFY
   // Measurement build only (variants/libedv_noverify.so, loaded by bench.py's
   // C5 leg through EDV_LIB in a separate process, never the product library):
@@ -641,7 +659,8 @@ int launch_main(const VerifyArgs& va, hipStream_t s) {
   return 0;
 #endif
   const unsigned blocks = unsigned((va.n + kBlock - 1) / kBlock);
-  edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
+  if (prio) edv_main_kernel_prio<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
+  else edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(va);
   HIPOK(hipGetLastError(), "main launch");
   return 0;
 }
@@ -753,7 +772,7 @@ int launch_pipelined(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, con
       HIPOK(hipEventRecord(c.prep_done[b], c.sp), "record");
       if ((err = launch_prep_sides(vp, c.sm))) return err;
       HIPOK(hipStreamWaitEvent(c.sm, c.prep_done[b], 0), "wait");
-      if ((err = launch_main(va, c.sm))) return err;
+      if ((err = launch_main(va, c.sm, true))) return err;
       HIPOK(hipEventRecord(c.main_done[b], c.sm), "record");
       c.pending[b] = true;
       continue;

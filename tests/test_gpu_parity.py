@@ -254,9 +254,13 @@ def test_device_mask_selects_device():
         edv.verify_arrays(sigs, pks, msgs, off, device_mask=1 << 20)
 
 
-def test_pipelined_submission_matches():
+@pytest.mark.parametrize("flags", [0, edv.FLAG_SPLIT_PREP, edv.FLAG_SPLIT_PREP | edv.FLAG_UNIFORM_LENGTH])
+def test_pipelined_submission_matches(flags):
     """edv_verify_batch_dev_pipelined: several different batches in flight on the
-    two-stream pipeline (state sets alternate) give each batch its own verdicts."""
+    two-stream pipeline (state sets alternate) give each batch its own verdicts;
+    also with the split prep (EDV_FLAG_SPLIT_PREP: the hash side of batch k+1
+    beside the main kernel of batch k, the point sides on the main stream), with
+    and without length buckets."""
     batches = []
     for k in range(5):
         sigs, pks, msgs, off = orc.corpus(0x919 + k, 0, 1500 + 300 * k, mode=k % 2, invalid_permille=150)
@@ -270,7 +274,8 @@ def test_pipelined_submission_matches():
         edv.set_chunk(0, 1024)  # several chunks per batch: the pipeline alternates within a batch too
         for _ in range(2):
             for bufs, acc, want in batches:
-                edv.verify_device_pipelined(bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, len(want), acc.ptr)
+                edv.verify_device_pipelined(bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, len(want), acc.ptr,
+                                            flags=flags)
             edv.pipeline_sync(0)
             for bufs, acc, want in batches:
                 assert np.array_equal(acc.download(len(want)), want)

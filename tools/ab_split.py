@@ -22,6 +22,7 @@ s = edv.stream(dev)
 batches = {"C2": workload.DeviceBatch(65536, device=dev),
            "C4": workload.DeviceBatch(65536, device=dev, seed=0xC4C4, var_range=(200, 4096), damage_every=20,
                                       damage_kinds=7, keep_host=False)}
+MODES = os.environ.get("MODES", "sequential,pipelined,split").split(",")
 modes = {"sequential": (lambda b: b.verify(stream=s), lambda: edv.sync(dev)),
          "pipelined": (lambda b: b.submit(), lambda: edv.pipeline_sync(dev)),
          "split": (lambda b: b.submit(edv.FLAG_SPLIT_PREP), lambda: edv.pipeline_sync(dev))}
@@ -29,6 +30,8 @@ for rnd in range(ROUNDS):
     for name, b in batches.items():
         exp = b.expected()
         for mode, (step, drain) in modes.items():
+            if mode not in MODES:
+                continue
             for _ in range(10):
                 step(b)
             drain()
@@ -45,5 +48,5 @@ for rnd in range(ROUNDS):
                 drain()
                 reps.append((time.perf_counter() - t0) / STEPS)
             ms = 1e3 * statistics.median(reps)
-            print(json.dumps({"round": rnd, "config": name, "mode": mode, "ms_per_step": ms,
+            print(json.dumps({"lib": os.path.basename(edv.LIB_PATH), "round": rnd, "config": name, "mode": mode, "ms_per_step": ms,
                               "verifies_per_s": b.n / (ms * 1e-3), "verdicts_ok": ok}), flush=True)
