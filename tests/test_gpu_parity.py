@@ -224,6 +224,37 @@ def test_big_corpus_parity(name):
         assert mism.size == 0, (s, mism[:10].tolist())
 
 
+@pytest.mark.slow
+def test_big_corpus_split_pipeline():
+    """The split pipeline (EDV_FLAG_SPLIT_PREP, the C4 leg's fast mode) on the
+    whole c4_var corpus (1,048,576 requests of 200..4,096 B, 5 % invalid) against
+    libsodium's committed bitmask, in 65,536-request chunks as at C4: every
+    chunk's hash side runs beside the previous chunk's main kernel.
+    EDV_PARITY_QUICK=1 runs the first 262,144 requests."""
+    meta = _bitmask_meta()
+    cfg = meta["corpora"]["c4_var"]
+    n = 262144 if os.environ.get("EDV_PARITY_QUICK") == "1" else cfg["count"]
+    sigs, pks, msgs, off = orc.corpus(cfg["seed"], 0, n, cfg["mode"], cfg["invalid_permille"])
+    bits = np.fromfile(os.path.join(GOLDEN, "corpus_c4_var.bits"), dtype=np.uint8)
+    want = np.unpackbits(bits[:n // 8], bitorder="little")
+    bufs = [edv.DeviceBuffer(a.nbytes + 64) for a in (sigs, pks, msgs, off)]
+    for b, a in zip(bufs, (sigs, pks, msgs, off)):
+        b.upload(a)
+    acc = edv.DeviceBuffer(n)
+    acc.upload(np.full(n, 7, np.uint8))
+    try:
+        edv.set_chunk(0, 65536)
+        for _ in range(2):   # the second pass runs with both state sets already in use
+            edv.verify_device_pipelined(bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, n, acc.ptr,
+                                        flags=edv.FLAG_SPLIT_PREP)
+        edv.pipeline_sync(0)
+    finally:
+        edv.set_chunk(0, 0)
+    got = acc.download(n)
+    mism = np.nonzero(got != want)[0]
+    assert mism.size == 0, mism[:10].tolist()
+
+
 def test_device_resident_entry_point():
     sigs, pks, msgs, off = orc.corpus(0xD1, 0, 3000, mode=1, invalid_permille=100)
     want = checker(sigs, pks, msgs, off)
