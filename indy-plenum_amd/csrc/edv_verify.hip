@@ -165,50 +165,54 @@ struct RegBTab {
 
 // Phase 2: V8 multi-scalar walk and the identity check.  The window count is
 // the wave's maximum over its live lanes, so the loop stays wave-uniform.
-__device__ __forceinline__ void main_body(const VerifyArgs& a, int32_t* lds_main) {
-  const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-  const bool live = j < a.n && a.st.alive[j] && a.st.alive[a.st.cap + j] && a.st.alive[2 * a.st.cap + j];
-  const uint32_t* d = a.st.dig + j;
-  const uint64_t cap = a.st.cap;
-  const uint32_t wf = live ? d[uint64_t(kDigNwin) * cap] : 0;
-  int nwin = int(wf & 0xff);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) nwin = max(nwin, __shfl_xor(nwin, o));
-  nwin = __builtin_amdgcn_readfirstlane(nwin);
-  if (!live) return;
-  const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
-  uint32_t da[8], db[8], bw[kBDigits];
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    da[k] = d[uint64_t(k) * cap];
-    db[k] = d[uint64_t(8 + k) * cap];
-  }
-#pragma unroll
-  for (int k = 0; k < kBDigits; k++) bw[k] = d[uint64_t(kDigB + k) * cap];
-  // Settle the digit loads here, once: the digit registers are shifted inside
-  // the window loop, and the waitcnt pass, merging the loop's back edge with
-  // loads still pending from the preheader, otherwise inserts vmcnt waits at
-  // the loop head and right after the B-table loads (so every fourth window
-  // stalled on its table reads; 9.5 % of wave cycles in SQ_WAIT_ANY).
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    da[k] = uint32_t(opaque_i32(int32_t(da[k])));
-    db[k] = uint32_t(opaque_i32(int32_t(db[k])));
-  }
-#pragma unroll
-  for (int k = 0; k < kBDigits; k++) bw[k] = uint32_t(opaque_i32(int32_t(bw[k])));
-  int32_t* wl = lds_main + (threadIdx.x >> 6) * kLdsWaveWords;
-  const int lane = int(threadIdx.x & 63);
-  LdsATab at{a.st.atab + j * kAWords, wl, lane}, rt{a.st.rtab + j * kAWords, wl + kLdsAWords, lane};
+// The main kernel's body, shared by edv_main_kernel and the split pipeline's
+// edv_main_kernel_prio as a macro (text, not a function), so the plain kernel
+// compiles exactly as it did alone: an inlined-function form measured 2 %
+// slower at C2 (other register assignment; profiles/r04/ab_refactor_s11.jsonl).
 #ifndef EDV_MAIN_BLDS
-  RegBTab bt{a.btab, {0, 0}, {}};
+#define EDV_MAIN_BTAB RegBTab bt{a.btab, {0, 0}, {}};
 #else
-  LdsBTab bt{a.btab, wl + 2 * kLdsAWords, lane};
+#define EDV_MAIN_BTAB LdsBTab bt{a.btab, wl + 2 * kLdsAWords, lane};
 #endif
-  MAIN_STAMP(1);
-  a.accept[i] = main_one(da, db, bw, nwin, (wf >> 8) & 1, at, rt, bt) ? 1 : 0;
+// (In the body: the digit loads are settled once, through opaque_i32, before
+// the window loop: the digit registers are shifted inside the loop, and the
+// waitcnt pass, merging the loop's back edge with loads still pending from the
+// preheader, otherwise inserts vmcnt waits at the loop head and right after
+// the B-table loads, so every fourth window stalled on its table reads.)
+#define EDV_MAIN_BODY \
+  const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x; \
+  const bool live = j < a.n && a.st.alive[j] && a.st.alive[a.st.cap + j] && a.st.alive[2 * a.st.cap + j]; \
+  const uint32_t* d = a.st.dig + j; \
+  const uint64_t cap = a.st.cap; \
+  const uint32_t wf = live ? d[uint64_t(kDigNwin) * cap] : 0; \
+  int nwin = int(wf & 0xff); \
+_Pragma("unroll") \
+  for (int o = 32; o > 0; o >>= 1) nwin = max(nwin, __shfl_xor(nwin, o)); \
+  nwin = __builtin_amdgcn_readfirstlane(nwin); \
+  if (!live) return; \
+  const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j); \
+  uint32_t da[8], db[8], bw[kBDigits]; \
+_Pragma("unroll") \
+  for (int k = 0; k < 8; k++) { \
+    da[k] = d[uint64_t(k) * cap]; \
+    db[k] = d[uint64_t(8 + k) * cap]; \
+  } \
+_Pragma("unroll") \
+  for (int k = 0; k < kBDigits; k++) bw[k] = d[uint64_t(kDigB + k) * cap]; \
+_Pragma("unroll") \
+  for (int k = 0; k < 8; k++) { \
+    da[k] = uint32_t(opaque_i32(int32_t(da[k]))); \
+    db[k] = uint32_t(opaque_i32(int32_t(db[k]))); \
+  } \
+_Pragma("unroll") \
+  for (int k = 0; k < kBDigits; k++) bw[k] = uint32_t(opaque_i32(int32_t(bw[k]))); \
+  int32_t* wl = lds_main + (threadIdx.x >> 6) * kLdsWaveWords; \
+  const int lane = int(threadIdx.x & 63); \
+  LdsATab at{a.st.atab + j * kAWords, wl, lane}, rt{a.st.rtab + j * kAWords, wl + kLdsAWords, lane}; \
+  EDV_MAIN_BTAB \
+  MAIN_STAMP(1); \
+  a.accept[i] = main_one(da, db, bw, nwin, (wf >> 8) & 1, at, rt, bt) ? 1 : 0; \
   MAIN_STAMP(15);
-}
 
 __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   __shared__ int32_t lds_main[(kBlock / 64) * kLdsWaveWords];
@@ -216,7 +220,7 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   return;
 #endif
   MAIN_STAMP(0);
-  main_body(a, lds_main);
+  EDV_MAIN_BODY
 }
 
 // The split pipeline's main kernel (EDV_FLAG_SPLIT_PREP): the same walk at a
@@ -230,7 +234,7 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
 __global__ __launch_bounds__(kBlock) void edv_main_kernel_prio(VerifyArgs a) {
   __shared__ int32_t lds_main[(kBlock / 64) * kLdsWaveWords];
   __builtin_amdgcn_s_setprio(EDV_SPLIT_MAIN_PRIO);
-  main_body(a, lds_main);
+  EDV_MAIN_BODY
 }
 
 // Comb rows for the batch signer, in global memory (528 KB, L2-resident).
