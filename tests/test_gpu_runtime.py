@@ -180,15 +180,15 @@ def _pinned_copy(sigs, pks, msgs, off, n):
 
 def test_host_async_path():
     """edv_verify_batch_async / edv_wait_async: batches of fixed and mixed
-    lengths (sizes 20,000 / 4,097 / 65,536 / 1 / 30,000, 15 % invalid) queued
-    back to back from pageable memory, twice over (ten in flight: slots reused
-    without an explicit wait, the submission completing the batch eight back),
-    then pinned inputs with pinned verdict buffers in turn; every batch equals
-    the checker."""
-    sizes = (20000, 4097, 65536, 1, 30000)
+    lengths (sizes 20,000 / 4,097 / 65,536 / 1 / 30,000 / 40,000, 15 % invalid)
+    queued back to back from pageable memory, twice over (twelve in flight:
+    slots reused without an explicit wait, the submission completing the batch
+    eight back), then pinned inputs with pinned verdict buffers in turn; every
+    batch equals the checker."""
+    sizes = (20000, 4097, 65536, 1, 30000, 40000)
     batches = [orc.corpus(0xA5A0 + k, 0, n, mode=k % 2, invalid_permille=150) for k, n in enumerate(sizes)]
     wants = [checker(*b) for b in batches]
-    order = list(range(5)) * 2
+    order = list(range(6)) * 2
     accs = [np.full(sizes[k], 7, np.uint8) for k in order]
     tickets = []
     for j, k in enumerate(order):
