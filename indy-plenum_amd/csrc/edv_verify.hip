@@ -958,6 +958,75 @@ int run_shard_split(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const ui
   return 0;
 }
 
+// A shard of one chunk, copied field by field (the default host path for a
+// shard that fits one chunk).  Splitting the copy by requests cannot help: a
+// sub-batch's kernels take a whole batch's time (latency-bound lanes, DESIGN.md
+// section 3).  Splitting it by input field can: the two point sides need only
+// the signatures (R) and keys (A), 27 % of the bytes, and the hash side only
+// runs after the messages (71 %) land.  So: H2D of sigs, pks and offsets, then
+// of the messages, on the copy stream; the point sides (and the length buckets)
+// start on stream hs[0] as soon as the first part is in, while the messages
+// still copy; the hash side on hs[1] once they are in; the main kernel on hs[0]
+// after both; then the verdicts' D2H.  Caller holds c.mu.
+int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
+                     uint64_t lo, uint64_t hi, bool pinned, bool varied, uint8_t* d_sigs, uint8_t* d_pks,
+                     uint8_t* d_msgs, uint64_t* d_off, uint8_t* d_acc, uint8_t* h_acc) {
+  const uint64_t n = hi - lo, mbase = off[lo], mbytes = off[hi] - mbase;
+  const hipStream_t cp = c.hcp, s0 = c.hs[0], s1 = c.hs[1];
+  // the scratch's previous users (any stream) finish before the kernels write it,
+  // and the copies follow the previous call's
+  HIPOK(hipStreamWaitEvent(cp, c.st_done, 0), "wait scratch");
+  HIPOK(hipStreamWaitEvent(s0, c.st_done, 0), "wait scratch");
+  HIPOK(hipStreamWaitEvent(s1, c.st_done, 0), "wait scratch");
+  const uint8_t *src_s = sigs + 64 * lo, *src_p = pks + 32 * lo, *src_m = msgs + mbase;
+  const uint8_t* src_o = reinterpret_cast<const uint8_t*>(off + lo);
+  PinnedBuf& sl = c.stage[0];
+  if (!pinned) {
+    HIPOK(hipEventSynchronize(c.hs_staged[0]), "stage wait");  // the slot's previous H2D is done
+    if (sl.ensure(n * 96 + (n + 1) * 8 + mbytes)) return EDV_E_OOM;
+    uint8_t* p = static_cast<uint8_t*>(sl.p);
+    par_copy({{p, src_s, 64 * n}, {p + 64 * n, src_p, 32 * n}, {p + 96 * n, src_o, 8 * (n + 1)}});
+    src_s = p; src_p = p + 64 * n; src_o = p + 96 * n;
+  }
+  HIPOK(hipMemcpyAsync(d_sigs, src_s, n * 64, hipMemcpyHostToDevice, cp), "h2d sigs");
+  HIPOK(hipMemcpyAsync(d_pks, src_p, n * 32, hipMemcpyHostToDevice, cp), "h2d pks");
+  HIPOK(hipMemcpyAsync(d_off, src_o, (n + 1) * 8, hipMemcpyHostToDevice, cp), "h2d off");
+  HIPOK(hipEventRecord(c.part_copied[0], cp), "record");
+  if (!pinned) {
+    // stage the messages while the first part's DMA and the point sides run
+    uint8_t* pm = static_cast<uint8_t*>(sl.p) + 96 * n + 8 * (n + 1);
+    par_copy({{pm, src_m, mbytes}});
+    src_m = pm;
+  }
+  if (mbytes) HIPOK(hipMemcpyAsync(d_msgs, src_m, mbytes, hipMemcpyHostToDevice, cp), "h2d msgs");
+  HIPOK(hipEventRecord(c.part_copied[1], cp), "record");
+  if (!pinned) HIPOK(hipEventRecord(c.hs_staged[0], cp), "record");
+  const bool bucket = bucketing_enabled(c, varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH);
+  VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, mbase, d_acc, bucket);
+  va.n = n;
+  int err;
+  HIPOK(hipStreamWaitEvent(s0, c.part_copied[0], 0), "wait copy");
+  if (bucket && (err = launch_buckets(bucket_ctr(c.st, 0), va, d_off, s0))) return err;
+  HIPOK(hipEventRecord(c.part_prepped[0], s0), "record");  // the bucket permutation is written
+  VerifyArgs vp = va, vh = va;
+  vp.side0 = 1;
+  vp.nsides = 2;
+  vh.side0 = 0;
+  vh.nsides = 1;
+  if ((err = launch_prep_sides(vp, s0))) return err;
+  HIPOK(hipStreamWaitEvent(s1, c.part_copied[1], 0), "wait copy");
+  HIPOK(hipStreamWaitEvent(s1, c.part_prepped[0], 0), "wait buckets");
+  if ((err = launch_prep_sides(vh, s1))) return err;
+  HIPOK(hipEventRecord(c.part_prepped[1], s1), "record");
+  HIPOK(hipStreamWaitEvent(s0, c.part_prepped[1], 0), "wait hash side");
+  if ((err = launch_main(va, s0))) return err;
+  HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, s0), "d2h accept");
+  HIPOK(hipEventRecord(c.st_done, s0), "record scratch");
+  HIPOK(hipStreamWaitEvent(c.stream, c.st_done, 0), "join");
+  HIPOK(hipStreamSynchronize(s0), "stream sync");
+  return 0;
+}
+
 // One shard on one device, host buffers: sub-batches of P requests go round
 // robin over the kQ host-path streams; per sub-batch: H2D copies (straight
 // from the caller's memory when it is pinned, else through this stream's
@@ -1007,6 +1076,16 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
     if (c.off.ensure((n + parts) * 8)) return EDV_E_OOM;
     if ((err = run_shard_split(c, sigs, pks, msgs, off, lo, hi, parts, pinned, d_sigs, d_pks, d_msgs,
                                static_cast<uint64_t*>(c.off.p), d_acc, h_acc)))
+      return err;
+    if (!acc_pinned) memcpy(accept + lo, h_acc, n);
+    return 0;
+  }
+  // One chunk: copied field by field, the point sides starting before the
+  // messages are in (EDV_HOST_FIELDS=0 restores the one-sub-batch path for A/B).
+  const char* fe = getenv("EDV_HOST_FIELDS");
+  if (nsub == 1 && !(fe && atoi(fe) == 0)) {
+    if ((err = run_shard_fields(c, sigs, pks, msgs, off, lo, hi, pinned, varied, d_sigs, d_pks, d_msgs, d_off,
+                                d_acc, h_acc)))
       return err;
     if (!acc_pinned) memcpy(accept + lo, h_acc, n);
     return 0;
