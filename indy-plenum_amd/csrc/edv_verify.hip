@@ -858,6 +858,44 @@ void par_copy(const std::vector<Seg>& segs) {
   for (auto& x : th) x.join();
 }
 
+// memcpy of `bytes` into pinned staging, in K chunks over copy_threads()
+// threads, with chunk k's DMA to the device queued on stream s as soon as every
+// thread has copied its part of it, so the staging of chunk k+1 overlaps the
+// DMA of chunk k (pageable inputs of a synchronous call: the messages, 71 % of
+// a C2 batch's bytes).  Below 8 MiB: one par_copy, one DMA.
+int stage_and_send(uint8_t* dev, uint8_t* stage, const uint8_t* src, uint64_t bytes, hipStream_t s) {
+  if (bytes < (uint64_t(8) << 20)) {
+    par_copy({{stage, src, bytes}});
+    HIPOK(hipMemcpyAsync(dev, stage, bytes, hipMemcpyHostToDevice, s), "h2d");
+    return 0;
+  }
+  constexpr int K = 4;
+  const int T = copy_threads();
+  std::atomic<int> done[K];
+  for (auto& d : done) d.store(0);
+  auto part = [&](int t) {
+    for (int k = 0; k < K; k++) {
+      const uint64_t c0 = bytes * k / K, c1 = bytes * (k + 1) / K;
+      const uint64_t a = c0 + (c1 - c0) * t / T, b = c0 + (c1 - c0) * (t + 1) / T;
+      memcpy(stage + a, src + a, b - a);
+      done[k].fetch_add(1, std::memory_order_release);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back(part, t);
+  int err = 0;
+  for (int k = 0; k < K; k++) {
+    const uint64_t c0 = bytes * k / K, c1 = bytes * (k + 1) / K;
+    const uint64_t a = c0, b = c0 + (c1 - c0) / T;
+    memcpy(stage + a, src + a, b - a);  // thread 0's part of chunk k
+    while (done[k].load(std::memory_order_acquire) < T - 1) std::this_thread::yield();
+    if (!err && hipMemcpyAsync(dev + c0, stage + c0, c1 - c0, hipMemcpyHostToDevice, s) != hipSuccess)
+      err = set_err(EDV_E_HIP, "h2d chunk");
+  }
+  for (auto& x : th) x.join();
+  return err;
+}
+
 uint64_t sha512_blocks(const uint64_t* off, uint64_t i) { return (64 + (off[i + 1] - off[i]) + 17 + 127) / 128; }
 // One branch-free pass over the offsets of requests [lo, hi): are they
 // non-decreasing, and do all messages have request lo's SHA-512 block count?
@@ -992,19 +1030,20 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
   HIPOK(hipMemcpyAsync(d_pks, src_p, n * 32, hipMemcpyHostToDevice, cp), "h2d pks");
   HIPOK(hipMemcpyAsync(d_off, src_o, (n + 1) * 8, hipMemcpyHostToDevice, cp), "h2d off");
   HIPOK(hipEventRecord(c.part_copied[0], cp), "record");
+  int err;
   if (!pinned) {
-    // stage the messages while the first part's DMA and the point sides run
+    // stage the messages while the first part's DMA and the point sides run,
+    // each quarter's DMA queued as soon as it is staged
     uint8_t* pm = static_cast<uint8_t*>(sl.p) + 96 * n + 8 * (n + 1);
-    par_copy({{pm, src_m, mbytes}});
-    src_m = pm;
+    if (mbytes && (err = stage_and_send(d_msgs, pm, src_m, mbytes, cp))) return err;
+  } else if (mbytes) {
+    HIPOK(hipMemcpyAsync(d_msgs, src_m, mbytes, hipMemcpyHostToDevice, cp), "h2d msgs");
   }
-  if (mbytes) HIPOK(hipMemcpyAsync(d_msgs, src_m, mbytes, hipMemcpyHostToDevice, cp), "h2d msgs");
   HIPOK(hipEventRecord(c.part_copied[1], cp), "record");
   if (!pinned) HIPOK(hipEventRecord(c.hs_staged[0], cp), "record");
   const bool bucket = bucketing_enabled(c, varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH);
   VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, mbase, d_acc, bucket);
   va.n = n;
-  int err;
   HIPOK(hipStreamWaitEvent(s0, c.part_copied[0], 0), "wait copy");
   if (bucket && (err = launch_buckets(bucket_ctr(c.st, 0), va, d_off, s0))) return err;
   HIPOK(hipEventRecord(c.part_prepped[0], s0), "record");  // the bucket permutation is written
