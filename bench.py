@@ -783,10 +783,11 @@ def main():
     iters = max(3, min(args.steps, 10))
     prep_ms, main_ms = edv.profile_device(batch.d_sigs.ptr, batch.d_pks.ptr, batch.d_msgs.ptr, batch.d_off.ptr, pn,
                                           batch.d_accept.ptr, dev, iters)
-    # untimed: every rank verifies once more, copies its accept bytes D2H and
-    # sends them to rank 0, which places each in its slice of one host array
+    # untimed: every rank verifies once more, packs its verdicts into a bitmask
+    # on the device (N/8 bytes), copies it D2H and sends it to rank 0, which
+    # places each shard's bits in its slice of one host array
     batch.verify()
-    mine = batch.accept()
+    mine = batch.accept_bits()
     parts = rdv.gather(mine.tobytes(), broadcast=False)
     verdicts_ok = None
     if rank == 0:
@@ -794,7 +795,9 @@ def main():
         bounds = ([shard.shard_range(total, world, r)[0] for r in range(world)] + [total] if c3
                   else [r * args.batch for r in range(world + 1)])
         for r, p in enumerate(parts):
-            full[bounds[r]:bounds[r + 1]] = np.frombuffer(p, np.uint8)
+            k = bounds[r + 1] - bounds[r]
+            full[bounds[r]:bounds[r + 1]] = np.unpackbits(np.frombuffer(p, np.uint8), bitorder="little")[:k]
+        gathered_bytes = sum(len(p) for p in parts)
         exp = np.ones(total, np.uint8)
         exp[workload.damage_positions(0, total, damage)] = 0
         verdicts_ok = bool(np.array_equal(full, exp))
@@ -827,12 +830,14 @@ def main():
                                                    "other ranks idle at a barrier, before the joint repetitions"
                                                    % (n, args.steps),
                      "scaling_efficiency": value / (world * one_gpu),
+                     "gathered": "accept bitmask, %d bytes from %d ranks (packed on each GPU, D2H, loopback TCP to "
+                                 "rank 0, after the timed region)" % (gathered_bytes, world),
                      "gpu_isolation": ("HIP_VISIBLE_DEVICES=<the LOCAL_RANK-th device> per rank" if own_gpu is not None
                                        else "EDV_VIRTUAL_DEVICES=%s: logical devices sharing the visible GPU(s) "
                                             "(rehearsal)" % os.environ.get("EDV_VIRTUAL_DEVICES"))}
     if c3:
         config = {"workload": "C3: %d Ed25519 verifies per step split by request index over %d GPU(s) (%d per GPU), "
-                              "fixed %d-byte serialized requests, 5 %% invalid, accept bytes gathered to host and "
+                              "fixed %d-byte serialized requests, 5 %% invalid, accept bitmask gathered to host and "
                               "checked" % (total, world, n, args.msg_len),
                   "total_per_step": total, "per_gpu": n, "msg_len": args.msg_len,
                   "parallelism": "shard-by-request-index x%d (one process per GPU)" % world}

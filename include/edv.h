@@ -228,6 +228,14 @@ int edv_device_count(void);
  * per prod (plenum/server/node.py:1026-1049, stp_core/config.py:28).
  */
 int edv_pick_device(uint32_t device_mask);
+
+/*
+ * Accept bytes -> accept bitmask on the device: d_bits[i / 8] bit (i % 8) =
+ * (d_accept[i] != 0), ceil(n / 8) bytes (numpy.packbits(..., bitorder="little")).
+ * What a multi-GPU run gathers to the host: N/8 bytes per shard.
+ * Asynchronous on `stream` if given, else synchronous on the library stream.
+ */
+int edv_pack_bits_dev(const uint8_t *d_accept, uint64_t n, uint8_t *d_bits, int device, void *stream);
 int edv_context_count(void);
 
 /*

@@ -331,6 +331,26 @@ __global__ __launch_bounds__(kBlock) void edv_bucket_scatter_kernel(const uint64
   if (j < n) perm[wbase[b] + rank] = uint32_t(j);
 }
 
+// Accept bytes -> accept bitmask (bit i % 8 of byte i / 8, little-endian bit
+// order): what a multi-GPU run gathers, N/8 bytes per shard.
+// One output byte per thread, its eight accept bytes read as two words when
+// they are whole.
+__global__ __launch_bounds__(kBlock) void edv_pack_bits_kernel(const uint8_t* acc, uint64_t n, uint8_t* bits) {
+  const uint64_t k = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (8 * k >= n) return;
+  uint32_t b = 0;
+  if (8 * k + 8 <= n && !(reinterpret_cast<uintptr_t>(acc) & 3)) {
+    const uint32_t lo = reinterpret_cast<const uint32_t*>(acc)[2 * k], hi = reinterpret_cast<const uint32_t*>(acc)[2 * k + 1];
+#pragma unroll
+    for (int t = 0; t < 4; t++) b |= (((lo >> (8 * t)) & 0xff) != 0 ? 1u : 0u) << t;
+#pragma unroll
+    for (int t = 0; t < 4; t++) b |= (((hi >> (8 * t)) & 0xff) != 0 ? 1u : 0u) << (4 + t);
+  } else {
+    for (uint64_t i = 8 * k; i < n && i < 8 * k + 8; i++) b |= (acc[i] != 0 ? 1u : 0u) << (i - 8 * k);
+  }
+  bits[k] = uint8_t(b);
+}
+
 // j * B and j * 2^kBSplit B for j = 0..2^(kBBits-1) in affine precomp form, once per device
 __global__ void edv_btab_kernel(int32_t* out) {
   const int t = threadIdx.x + blockIdx.x * blockDim.x;
@@ -1592,6 +1612,20 @@ int edv_sha256_batch(const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, u
   return for_each_shard(msg_off, n, device_mask, [&](DevCtx& c, uint64_t lo, uint64_t hi) {
     return run_digest_shard(c, msgs, msg_off, lo, hi, out);
   });
+}
+
+int edv_pack_bits_dev(const uint8_t* d_accept, uint64_t n, uint8_t* d_bits, int device, void* stream) {
+  g_err.clear();
+  if (n == 0) return 0;
+  if (!d_accept || !d_bits) return set_err(EDV_E_ARG, "null pointer");
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : cl.c->stream;
+  const uint64_t nb = (n + 7) / 8;
+  edv_pack_bits_kernel<<<dim3(unsigned((nb + kBlock - 1) / kBlock)), dim3(kBlock), 0, s>>>(d_accept, n, d_bits);
+  HIPOK(hipGetLastError(), "pack bits launch");
+  if (!stream) HIPOK(hipStreamSynchronize(s), "stream sync");
+  return 0;
 }
 
 int edv_sha256_batch_dev(const uint8_t* d_msgs, const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n,

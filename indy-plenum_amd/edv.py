@@ -120,6 +120,8 @@ def lib():
         h.edv_context_count.restype = ctypes.c_int
         h.edv_pick_device.argtypes = [ctypes.c_uint32]
         h.edv_pick_device.restype = ctypes.c_int
+        h.edv_pack_bits_dev.argtypes = [vp, u64, vp, ctypes.c_int, vp]
+        h.edv_pack_bits_dev.restype = ctypes.c_int
         h.edv_dev_alloc.argtypes = [ctypes.c_int, u64, ctypes.POINTER(ctypes.c_void_p)]
         h.edv_dev_free.argtypes = [ctypes.c_int, vp]
         h.edv_h2d.argtypes = [ctypes.c_int, vp, vp, u64]
@@ -263,6 +265,11 @@ def sha256_batch(messages, device_mask: int = 0):
     off[1:] = np.cumsum([len(m) for m in messages])
     d = sha256_arrays(b"".join(messages), off, device_mask)
     return [bytes(r) for r in d]
+
+
+def pack_bits_device(d_accept, n, d_bits, device=0, stream=None):
+    """Device accept bytes -> bitmask (ceil(n/8) bytes, little-endian bit order)."""
+    _check(lib().edv_pack_bits_dev(d_accept, n, d_bits, device, stream))
 
 
 def sha256_device(d_msgs, d_off, n, d_out, device=0, msg_base=0, stream=None):

@@ -172,6 +172,7 @@ class DeviceBatch:
         self.d_pks = edv.DeviceBuffer(32 * n, device)
         self.d_sigs = edv.DeviceBuffer(64 * n, device)
         self.d_accept = edv.DeviceBuffer(max(n, 1), device)
+        self._bits = None               # device bitmask buffer (accept_bits)
         self.bad = damage_positions(start, n, damage_every)
         host = np.empty(int(off[-1]) + 64, dtype=np.uint8) if keep_host else None
         d_seeds = edv.DeviceBuffer(32 * min(n, SLICE) + 64, device)
@@ -247,6 +248,15 @@ class DeviceBatch:
         if self.n:
             edv._check(edv.lib().edv_d2h(self.device, out.ctypes.data, self.d_accept.ptr, self.n))
         return out
+
+    def accept_bits(self):
+        """The verdicts as a bitmask (packed on the device, ceil(n/8) bytes D2H):
+        bit i % 8 of byte i / 8 = verdict i."""
+        nb = (self.n + 7) // 8
+        if self._bits is None:
+            self._bits = edv.DeviceBuffer(max(nb, 1), self.device)
+        edv.pack_bits_device(self.d_accept.ptr, self.n, self._bits.ptr, self.device)
+        return self._bits.download(nb)
 
     def host_copy(self):
         """(sigs, pks, msgs, off) host arrays of this batch."""

@@ -534,3 +534,22 @@ def test_bench_two_gpus_under_torch_distributed_run():
     line = _bench(["--gpus", "2", "--total", "1048576"] + _QUICK, env=env, launcher=launcher)
     assert line["n_gpus"] == 2 and line["verdicts_as_expected"] is True
     assert line["timing"]["launch"] == "torch.distributed.run ranks"
+
+
+def test_pack_bits_matches_numpy():
+    """edv_pack_bits_dev (the bitmask a multi-GPU run gathers) equals
+    numpy.packbits(accept != 0, bitorder="little") for lengths around the 8-bit
+    and word seams, at an unaligned start and for verdict bytes other than 0/1."""
+    rng = np.random.default_rng(0xB175)
+    for n in (1, 7, 8, 9, 63, 64, 65, 1000, 65536 + 3):
+        for shift in (0, 1):
+            a = rng.integers(0, 2, size=n, dtype=np.uint8)
+            a[::13] *= 7                      # any nonzero byte is a 1
+            buf = edv.DeviceBuffer(n + 8)
+            host = np.zeros(n + 8, np.uint8)
+            host[shift:shift + n] = a
+            buf.upload(host)
+            out = edv.DeviceBuffer((n + 7) // 8)
+            edv.pack_bits_device(buf.ptr + shift, n, out.ptr)
+            got = out.download((n + 7) // 8)
+            assert np.array_equal(got, np.packbits(a != 0, bitorder="little")), (n, shift)
