@@ -10,7 +10,9 @@ tests/test_gpu_parity.py with fresh corpora of a different generator:
       (small-order R, non-canonical A, small-order A included)
 
   fuzz 2,097,152 requests of 256 B with random bit flips anywhere in sig, pk
-      or message, or a random R, S or A (host buffers through edv_verify_batch)
+      or message, or a random R, S or A (pageable host buffers through
+      edv_verify_batch, FUZZ_SLICE requests per call, default 2^18 = one chunk:
+      the field-ordered path with staged message quarters)
 
   python tools/parity_live_sodium.py [c3_total] [c4_total] [fuzz_total]
 Prints one JSON line per workload and a summary; exit status 1 on any mismatch.
@@ -65,8 +67,9 @@ def fuzz(total, seed=0xF022):
     rng = np.random.default_rng(seed)
     checked = mism = rejected = 0
     first_bad = None
-    for start in range(0, total, SLICE):
-        n = min(SLICE, total - start)
+    fslice = int(os.environ.get("FUZZ_SLICE", 1 << 18))   # one chunk: the field-ordered synchronous path
+    for start in range(0, total, fslice):
+        n = min(fslice, total - start)
         b = workload.DeviceBatch(n, start=start, seed=seed, keep_host=True)
         sigs, pks, msgs, off = b.host_copy()
         del b
