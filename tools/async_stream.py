@@ -4,7 +4,9 @@ B, 5 % invalid): a stream of K batches, waiting one batch behind, per-batch
 time as the median of R streams; EDV_ASYNC_SPLIT unset (auto: the split
 pipeline from a mean of 6 SHA-512 blocks), 0 (off) and 1 (on); verdicts checked
 on every stream.  Also the device-resident sequential step for reference.
-Measurement only."""
+Measurement only.(EDV_ASYNC_SPLIT was removed from the library after this measurement,
+profiles/r04/async_stream_s13.jsonl; with HEAD all three rows take the ordinary path.)
+"""
 import json
 import os
 import statistics

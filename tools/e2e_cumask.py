@@ -4,7 +4,9 @@ confined to its own 1/Q of the CUs (EDV_HOST_CUMASK modes 1-3, see
 host_streams in csrc/edv_verify.hip), and the zero-copy form (cfg suffix :z,
 EDV_ZERO_COPY: the kernels read the pinned inputs over the link, no H2D copy).  Median of R calls back to back, and of
 R calls 5 ms apart (the GPU idles in between, as a Node's calls would).
-Verdicts checked on every configuration.  Measurement only."""
+Verdicts checked on every configuration.  Measurement only.(The CU-mask and zero-copy knobs were removed from the library after this
+measurement, profiles/r04/e2e_sync_variants_s2.jsonl; with HEAD they are ignored.)
+"""
 import json
 import os
 import statistics

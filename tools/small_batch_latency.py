@@ -3,7 +3,9 @@ from pinned host buffers: a synchronous edv_verify_batch call, and an
 edv_verify_batch_async submission + edv_wait_async, each with the DMA copies
 (default) and zero-copy (EDV_ZERO_COPY=1: the kernels read the pinned inputs
 and write the pinned verdicts over the link).  Median of R calls; verdicts
-checked.  Measurement only."""
+checked.  Measurement only.(EDV_ZERO_COPY was removed from the library after this measurement,
+profiles/r04/small_batch_latency_s2.jsonl; with HEAD both rows take the copy path.)
+"""
 import json
 import os
 import statistics
