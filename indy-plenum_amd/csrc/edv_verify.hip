@@ -828,6 +828,18 @@ int drain(DevCtx& c) {
   return 0;
 }
 
+// Best effort after a failed host-path call: wait for whatever was already
+// queued on the context's streams (copies may still read the caller's pinned
+// buffers), so no DMA touches them after the error is returned.
+void quiesce(DevCtx& c) {
+  hipStream_t ss[] = {c.stream, c.hcp, c.hac, c.sp, c.sm};
+  for (hipStream_t x : ss)
+    if (x) (void)hipStreamSynchronize(x);
+  for (int q = 0; q < kQ; q++)
+    if (c.hs[q]) (void)hipStreamSynchronize(c.hs[q]);
+  (void)hipGetLastError();
+}
+
 // ---- host memory: pinned detection and a parallel staging copy
 bool is_pinned(const void* p) {
   if (!p) return false;
@@ -1452,7 +1464,9 @@ int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard 
     Inflight inf(g_ctx[dev]);
     CtxLock cl(dev);
     if (cl.err) return cl.err;
-    return shard(*cl.c, lo, hi);
+    const int rc = shard(*cl.c, lo, hi);
+    if (rc) quiesce(*cl.c);
+    return rc;
   };
   if (g == 1) return one(pick_device(devs), 0, n);
   devs.resize(g);
