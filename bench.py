@@ -663,6 +663,26 @@ def c4_leg(dev, steps, reps, n=65536):
                                         "main"}}
 
 
+def c3_shard_leg(dev, steps, reps, world_max=8):
+    """The same-workload one-GPU reference for the driver's 1 -> 8 GPU curve: one
+    rank's C3 shard at N = 8 (16,777,216 / 8 = 2,097,152 requests of 256 B, 5 %
+    damaged, walked in 2^18-request launches), timed on this one GPU.  The N = 1
+    line is C2 (65,536 per step), so value(N) / (N x this) is the curve's
+    same-workload efficiency."""
+    from indy_plenum_amd import edv, shard, workload
+    lo, hi = shard.shard_range(C3_TOTAL, world_max, 0)
+    b = workload.DeviceBatch(hi - lo, device=dev, start=lo, damage_every=C3_DAMAGE_EVERY, keep_host=False)
+    b.verify()
+    ok = bool(np.array_equal(b.accept(), b.expected()))
+    s = edv.stream(dev)
+    ts = timed_steps(lambda: b.verify(stream=s), lambda: edv.sync(dev), max(1, steps // 4), reps, Rendezvous(0, 1, ""))
+    el = statistics.median(ts)
+    return {"workload": "C3's shard at N = %d: %d requests of 256 B per step on one GPU, 5 %% damaged"
+                        % (world_max, b.n),
+            "verifies_per_s": b.n * max(1, steps // 4) / el, "reps_s": ts, "verdicts_as_expected": ok,
+            "use": "same-workload reference for value(N) / (N x verifies_per_s) over --gpus 1, 2, 4, 8"}
+
+
 def c5_leg(n=20000, n_cpu=2000):
     """C5 (BASELINE configs[4]): the 4-node pool (Alpha..Delta) under a client
     flood with the GPU verify_batch behind ReqAuthenticator, against the
@@ -822,7 +842,8 @@ def main():
         roofline.update(pmc)
     if world > 1:
         one_gpu = n * args.steps / alone   # rank 0's shard, timed alone
-        out_multi = {"per_rank_s": per_rank_s, "slowest_rank": int(np.argmax(per_rank_s)),
+        out_multi = {"per_gpu_verifies_per_s": value / world,
+                     "per_rank_s": per_rank_s, "slowest_rank": int(np.argmax(per_rank_s)),
                      "slowest_rank_s": max(per_rank_s), "per_rank_what": "each rank's median repetition "
                      "(%d steps), its own clock between the barriers" % args.steps,
                      "one_gpu_same_workload_verifies_per_s": one_gpu,
@@ -880,7 +901,8 @@ def main():
         except Exception as ex:
             out["node_path"] = {"error": repr(ex)}
     if world == 1 and not c3 and not args.no_extra:
-        for name, leg in (("c4", lambda: c4_leg(dev, args.steps, args.reps)), ("c5", c5_leg)):
+        for name, leg in (("c3_shard", lambda: c3_shard_leg(dev, args.steps, args.reps)),
+                          ("c4", lambda: c4_leg(dev, args.steps, args.reps)), ("c5", c5_leg)):
             try:
                 out[name] = leg()
             except Exception as ex:
