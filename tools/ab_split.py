@@ -19,9 +19,13 @@ from indy_plenum_amd import edv, workload  # noqa: E402
 STEPS, REPS, ROUNDS = (int(os.environ.get(k, d)) for k, d in (("STEPS", 20), ("REPS", 5), ("ROUNDS", 2)))
 dev = 0
 s = edv.stream(dev)
-batches = {"C2": workload.DeviceBatch(65536, device=dev),
-           "C4": workload.DeviceBatch(65536, device=dev, seed=0xC4C4, var_range=(200, 4096), damage_every=20,
-                                      damage_kinds=7, keep_host=False)}
+CONFIGS = os.environ.get("CONFIGS", "C2,C4").split(",")
+batches = {}
+if "C2" in CONFIGS:
+    batches["C2"] = workload.DeviceBatch(65536, device=dev)
+if "C4" in CONFIGS:
+    batches["C4"] = workload.DeviceBatch(65536, device=dev, seed=0xC4C4, var_range=(200, 4096), damage_every=20,
+                                         damage_kinds=7, keep_host=False)
 MODES = os.environ.get("MODES", "sequential,pipelined,split").split(",")
 modes = {"sequential": (lambda b: b.verify(stream=s), lambda: edv.sync(dev)),
          "pipelined": (lambda b: b.submit(), lambda: edv.pipeline_sync(dev)),
