@@ -523,6 +523,56 @@ def e2e_leg(batch, device_value, reps=5):
             "pcie_bytes_per_call": int(sigs.nbytes + pks.nbytes + off.nbytes + int(off[-1] - off[0]) + n)}
 
 
+def single_call_leg(calls=200):
+    """Batch-of-one through the GPU (INTEGRATION.md ways 1 and 2): one request per
+    call through nacl_wrappers.Verifier.verify (nacl_wrappers.py:232-242) and
+    through ReqAuthenticator.authenticate (req_authenticator.py:22-44), median of
+    `calls` calls each, next to the reference's per-call path on libsodium in the
+    same run (crypto_sign_open via ctypes, as libnacl; DidVerifier key derivation)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import sodium_ref
+    from indy_plenum_amd import base58
+    from indy_plenum_amd.client_authn import CoreAuthNr
+    from indy_plenum_amd.nacl_wrappers import Verifier
+    from indy_plenum_amd.req_authenticator import ReqAuthenticator
+    from indy_plenum_amd.signing_serializer import serialize_msg_for_signing
+    from indy_plenum_amd.verifier import DidVerifier
+    verkeys, reqs = c1_requests(1, seed=0x51)
+    req = reqs[0]
+    idr, vk = req["identifier"], verkeys[req["identifier"]]
+    sig = base58.b58decode(req["signature"])
+    msg = serialize_msg_for_signing({k: v for k, v in req.items() if k != "signature"})
+    pk = DidVerifier(vk, idr).batch_key()
+    v = Verifier(pk)
+    assert v.verify(sig, msg) and not v.verify(sig, msg + b"x")
+    auth = CoreAuthNr()
+    auth.addIdr(idr, vk)
+    ra = ReqAuthenticator()
+    ra.register_authenticator(auth)
+    assert ra.authenticate(req) == {idr}
+
+    def med_us(f):
+        for _ in range(5):
+            f()
+        return 1e6 * median_time(f, calls)
+    out = {"what": "one request per call, median of %d calls (after 5 warm calls); the GPU does every verify" % calls,
+           "verifier_verify_gpu_us": med_us(lambda: v.verify(sig, msg)),
+           "req_authenticator_gpu_us": med_us(lambda: ra.authenticate(req))}
+    if sodium_ref.sodium() is not None:
+        sv = sodium_ref.SodiumVerifier(vk, idr)
+        assert sv.verify(sig, msg)
+        out["verifier_verify_libsodium_us"] = med_us(lambda: sv.verify(sig, msg))
+        cpu = sodium_ref.SodiumCoreAuthNr()
+        cpu.addIdr(idr, vk)
+        rc = ReqAuthenticator()
+        rc.register_authenticator(cpu)
+        out["req_authenticator_libsodium_us"] = med_us(lambda: rc.authenticate(req))
+        out["verifier_gpu_over_libsodium_time"] = out["verifier_verify_gpu_us"] / out["verifier_verify_libsodium_us"]
+        out["note"] = ("a GPU batch of one pays a whole launch pair's latency (one serial chain per lane); "
+                       "callers verify per prod (INTEGRATION.md way 3), where one call carries hundreds of requests")
+    return out
+
+
 class DictState:
     """A state with the reference's get(key, isCommitted) contract
     (PruningState.get, state/pruning_state.py), held in a dict: the NYM values
@@ -851,6 +901,7 @@ def main():
                                                    "other ranks idle at a barrier, before the joint repetitions"
                                                    % (n, args.steps),
                      "scaling_efficiency": value / (world * one_gpu),
+                     "gathered_bytes": gathered_bytes,
                      "gathered": "accept bitmask, %d bytes from %d ranks (packed on each GPU, D2H, loopback TCP to "
                                  "rank 0, after the timed region)" % (gathered_bytes, world),
                      "gpu_isolation": ("HIP_VISIBLE_DEVICES=<the LOCAL_RANK-th device> per rank" if own_gpu is not None
@@ -884,6 +935,8 @@ def main():
         "config": config,
         "roofline": roofline,
         "verdicts_as_expected": verdicts_ok,
+        "inputs": "device-resident: the batch is in HBM before the timed region (the host-buffer boundary "
+                  "edv_verify_batch is timed in the e2e leg)",
         **({"multi_gpu": out_multi} if world > 1 else {}),
         "timing": {"mode": ("pipelined, split prep (hash side of step k+1 beside main of step k, point sides after "
                             "it)" if args.split_prep else "pipelined (prep of step k+1 beside main of step k)")
@@ -896,6 +949,11 @@ def main():
     }
     if world == 1 and not c3 and not args.no_e2e:
         out["e2e"] = e2e_leg(batch, value)
+        out["boundary_async_pinned_vs_headline"] = out["e2e"]["async_pinned_vs_device_resident"]
+        try:
+            out["single_call"] = single_call_leg()
+        except Exception as ex:
+            out["single_call"] = {"error": repr(ex)}
         try:
             out["node_path"] = node_path_leg()
         except Exception as ex:

@@ -80,7 +80,10 @@ int edv_verify_batch(const uint8_t *sigs, const uint8_t *pks, const uint8_t *msg
 int edv_verify_batch_async(const uint8_t *sigs, const uint8_t *pks, const uint8_t *msgs, const uint64_t *msg_off,
                            uint64_t n, uint8_t *accept, int device, int64_t *ticket);
 /* Wait for batch `ticket` of `device` and hand over its verdicts (0 at once if
- * it already was); EDV_E_ARG for a ticket never issued. */
+ * it already was); EDV_E_ARG for a ticket never issued.  Fails closed: `accept`
+ * is zeroed at submission (an unfilled buffer rejects), and once a batch has
+ * failed, every wait for a ticket at or below it that is no longer pending
+ * returns EDV_E_HIP, however many batches fail later. */
 int edv_wait_async(int device, int64_t ticket);
 /*
  * edv_verify_batch_async that also returns, when `digests` is not NULL, the
@@ -177,9 +180,28 @@ int edv_profile_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uin
                           const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept, int device,
                           int iters, float *ms_prep, float *ms_main);
 
+/*
+ * Measurement helper: edv_profile_batch_dev with, when flush_bytes > 0, a
+ * kernel between prep and main that reads and rewrites a flush_bytes buffer
+ * (larger than the 256 MiB Infinity Cache: the prep kernel's tables are
+ * evicted before main reads them); ms_flush = that kernel's time.  Tells the
+ * main kernel's DRAM sensitivity apart from its Infinity-Cache hits.
+ */
+int edv_profile_batch_dev_flush(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
+                                const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept,
+                                int device, int iters, uint64_t flush_bytes, float *ms_prep, float *ms_flush,
+                                float *ms_main);
+
 /* Signatures per prep/main kernel pair on `device` (0 = default 2^18; rounded
  * down to a multiple of 256).  Tuning/testing knob: verdicts never depend on it. */
 int edv_set_chunk(int device, uint64_t chunk);
+
+/* Message slices of a synchronous edv_verify_batch shard that fits one chunk
+ * (1..8; 0 = default 4): the messages are copied in that many slices by
+ * request, and each slice's SHA-512 / scalar side runs as soon as it has
+ * landed, so only the last slice's remains after the copy.  Tuning knob:
+ * verdicts never depend on it. */
+int edv_set_host_slices(int device, int slices);
 
 /* SHA-512 length buckets of the device paths (a counting sort of each chunk by
  * block count, so a wave of the prep kernel hashes equally long messages):
@@ -217,11 +239,14 @@ int edv_device_count(void);
  * of a whole MI355X: a smaller shard takes as long as a full one; EDV_MIN_SHARD
  * overrides), so a Node-sized batch (a prod of a few hundred requests, or one
  * Verifier.verify) runs whole on ONE device, on the calling thread, and no
- * other device is initialised.  That device is edv_pick_device's choice among
- * device_mask (0 = all): an initialised device with nothing in flight, else a
- * device not yet initialised (order starting at pid mod devices), else the
- * least-loaded one.  The Node's asynchronous path asks it for the device of
- * each submission (edv_verify_batch_async takes the device explicitly).
+ * other device is initialised.  Devices are chosen the same way for one shard
+ * and for 2..7 shards of a mid-sized batch: initialised devices with nothing
+ * running first, then devices not yet initialised (order starting at pid mod
+ * devices), then the least-loaded (load = synchronous calls placed there +
+ * asynchronous batches still running on the GPU, waited for or not); concurrent
+ * calls see each other's choices.  edv_pick_device returns that choice for one
+ * shard; the Node's asynchronous path asks it for the device of each
+ * submission (edv_verify_batch_async takes the device explicitly).
  * edv_pick_device returns that device's index (or a negative EDV_E_* code);
  * edv_context_count: devices whose context (streams, scratch, B table) exists.
  * Reference: the per-request call being placed, nacl_wrappers.py:232-242, made
@@ -233,7 +258,9 @@ int edv_pick_device(uint32_t device_mask);
  * Accept bytes -> accept bitmask on the device: d_bits[i / 8] bit (i % 8) =
  * (d_accept[i] != 0), ceil(n / 8) bytes (numpy.packbits(..., bitorder="little")).
  * What a multi-GPU run gathers to the host: N/8 bytes per shard.
- * Asynchronous on `stream` if given, else synchronous on the library stream.
+ * Asynchronous on `stream` if given, else synchronous on the library stream;
+ * either way ordered after every verify already launched on `device` (any
+ * stream, pipelined submissions included).
  */
 int edv_pack_bits_dev(const uint8_t *d_accept, uint64_t n, uint8_t *d_bits, int device, void *stream);
 int edv_context_count(void);

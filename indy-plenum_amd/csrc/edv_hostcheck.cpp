@@ -8,6 +8,7 @@
 #include <vector>
 #include "edv_verify_core.h"
 #include "edv_sha256.h"
+#include "edv_ledger.h"
 
 using namespace edv;
 
@@ -151,6 +152,14 @@ void hc_recode_bscalar(const uint8_t* s32, uint32_t* out9) {
   recode_bscalar(out9, s);
 }
 int hc_btab_entries() { return kBEntries; }
+// the asynchronous path's ticket ledger (edv_ledger.h): issue n tickets, fail
+// the listed ones, then report settled() for each query
+void hc_ledger(int64_t n, const int64_t* failed, int nf, const int64_t* queries, int nq, int* out) {
+  AsyncLedger l;
+  for (int64_t i = 0; i < n; i++) l.issue();
+  for (int k = 0; k < nf; k++) l.fail(failed[k]);
+  for (int k = 0; k < nq; k++) out[k] = l.settled(queries[k]);
+}
 // windows the packed radix-2^kAWin digits need (the prep kernel's per-lane count)
 int hc_digits_windows(const uint32_t* d8) { return digits5_windows(d8); }
 // packed signed digits of a 32-byte scalar at radix 2^bits: 4 (64 digits: the main

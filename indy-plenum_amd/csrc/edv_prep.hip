@@ -6,24 +6,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#ifdef EDV_STAMPS
-// Diagnostic build only (tools/stamps.py): lane 0 of every wave records
-// s_memtime at the phase boundaries marked EDV_STAMP in edv_verify_core.h
-// into its own debug buffer, 16 slots per wave; nothing else reads it.
-__device__ unsigned long long* g_prep_stamps;
-__device__ __forceinline__ void edv_stamp(int slot) {
-  __builtin_amdgcn_sched_barrier(0);
-  unsigned long long t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  if ((threadIdx.x & 63) == 0 && g_prep_stamps) {
-    const unsigned wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    g_prep_stamps[16ull * wave + slot] = t;
-  }
-}
-#define EDV_STAMP(slot) edv_stamp(slot)
-#endif
-
 #include "edv_kernels.h"
 
 namespace edv {
@@ -47,20 +29,13 @@ __device__ __forceinline__ void prep_point_side(const VerifyArgs& a, uint64_t j,
   const bool ok = prep_point(P, tab);
   a.st.alive[side * a.st.cap + j] = ok ? 1 : 0;
   if (!ok) a.accept[i] = 0;
-  EDV_STAMP(15);
 }
-#ifndef EDV_PREP_WAVES
-#define EDV_PREP_WAVES 3  // minimum waves per SIMD the prep kernel's register budget must allow (three sides)
-#endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EDV_PREP_WAVES, 8))) void edv_prep_kernel(
+// the register budget allows at least three waves per SIMD (the three sides)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void edv_prep_kernel(
     VerifyArgs a) {
-  EDV_STAMP(0);
   const uint32_t ns = uint32_t(a.nsides);
   const int side = a.side0 + int(blockIdx.x % ns);
   const uint64_t j = uint64_t(blockIdx.x / ns) * kBlock + threadIdx.x;  // slot within the chunk
-#ifdef EDV_AB_SIDES  // measurement-only variant (wrong verdicts): bit k set = run side k
-  if (!((EDV_AB_SIDES >> side) & 1)) return;
-#endif
   if (side != 0) {
     prep_point_side(a, j, side);
     return;
@@ -89,17 +64,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EDV_PREP
   } else {
     a.accept[i] = 0;
   }
-  EDV_STAMP(15);
 }
 
 }  // namespace
-
-#ifdef EDV_STAMPS
-hipError_t set_prep_stamps(void* buf) {
-  unsigned long long* p = static_cast<unsigned long long*>(buf);
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_prep_stamps), &p, sizeof p);
-}
-#endif
 
 hipError_t launch_prep_kernel(unsigned grid, hipStream_t s, const VerifyArgs& va) {
   edv_prep_kernel<<<dim3(grid), dim3(kBlock), 0, s>>>(va);

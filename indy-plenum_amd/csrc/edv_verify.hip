@@ -21,6 +21,7 @@
 #include <string.h>
 #include <stdlib.h>
 #include <stdio.h>
+#include <algorithm>
 #include <atomic>
 #include <mutex>
 #include <thread>
@@ -28,41 +29,13 @@
 #include <vector>
 #include <string>
 
-#ifdef EDV_STAMPS
-#define EDV_STAMP(slot) edv_main_stamp_fwd(slot)
-__device__ void edv_main_stamp_fwd(int slot);
-#endif
 #include "edv_verify_core.h"
 #include "edv_kernels.h"
 #include "edv_sha256.h"
+#include "edv_ledger.h"
 #include "../../include/edv.h"
 
 using namespace edv;
-
-#ifdef EDV_STAMPS
-// Diagnostic build only (tools/stamps.py): see edv_prep.hip.
-__device__ unsigned long long* g_main_stamps;
-__device__ __forceinline__ void edv_main_stamp(int slot) {
-  __builtin_amdgcn_sched_barrier(0);
-  unsigned long long t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  if ((threadIdx.x & 63) == 0 && g_main_stamps) {
-    const unsigned wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    g_main_stamps[16ull * wave + slot] = t;
-  }
-}
-#define MAIN_STAMP(slot) edv_main_stamp(slot)
-__device__ void edv_main_stamp_fwd(int slot) { edv_main_stamp(slot); }
-namespace edv { hipError_t set_prep_stamps(void* buf); }
-extern "C" int edv_debug_set_stamps(void* prep_buf, void* main_buf) {
-  unsigned long long* p = static_cast<unsigned long long*>(main_buf);
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_main_stamps), &p, sizeof p) != hipSuccess) return -3;
-  return edv::set_prep_stamps(prep_buf) == hipSuccess ? 0 : -3;
-}
-#else
-#define MAIN_STAMP(slot) ((void)0)
-#endif
 
 namespace {
 
@@ -73,20 +46,12 @@ namespace {
 // nothing of it sits in registers during the window's doublings; fetch()
 // waits for the copies and reads the lane's 16-byte pieces back.  Per wave:
 // A 10 KiB + R 10 KiB = 20 KiB (80 KiB per 256-thread workgroup); the B
-// entries go to registers (RegBTab), or with EDV_MAIN_BLDS through LDS as well
-// (+16 KiB per wave, one workgroup per CU).
+// entries go to registers (RegBTab), so two 256-thread workgroups fit a CU (2
+// waves/SIMD once a chunk has more than one wave per SIMD: main 5.5 % faster at
+// 2^18 signatures than with the B entries staged through LDS as well, the same
+// at 2^16, profiles/r03/ab_main_s8.jsonl).
 constexpr int kLdsAWords = 10 * 256;  // one cached entry: 10 pieces of 64 lanes x 4 words
-constexpr int kLdsBWords = 8 * 256;   // one B entry: 8 pieces (words 30, 31 are padding)
-#ifndef EDV_MAIN_BLDS
-// B entries in registers (RegBTab below): the wave's LDS slice holds only the A
-// and R entries, 20 KiB, so two 256-thread workgroups fit a CU (2 waves/SIMD
-// once a chunk has more than one wave per SIMD: main 5.5 % faster at 2^18
-// signatures, the same at 2^16, profiles/r03/ab_main_s8.jsonl).  EDV_MAIN_BLDS
-// builds the round-2 layout (B entries staged through LDS too, 36 KiB/wave).
 constexpr int kLdsWaveWords = 2 * kLdsAWords;
-#else
-constexpr int kLdsWaveWords = 2 * kLdsAWords + kBTables * kLdsBWords;
-#endif
 __device__ __forceinline__ void wait_staged() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 struct LdsATab {
   const int32_t* slot;  // this lane's table in global memory
@@ -113,28 +78,6 @@ struct LdsATab {
     }
     return c;
   }
-};
-struct LdsBTab {
-  const int32_t* w;  // both shared tables
-  int32_t* lds;      // kBTables x kLdsBWords
-  int lane;
-  __device__ __forceinline__ void stage(int tb, int j) {
-    const int32_t* g = w + (tb * kBEntries + j) * kBStride;
-#pragma unroll
-    for (int q = 0; q < 8; q++)
-      __builtin_amdgcn_global_load_lds(const_cast<int32_t*>(g + 4 * q), lds + tb * kLdsBWords + q * 256, 16, 0, 0);
-  }
-  __device__ __forceinline__ ge_precomp fetch(int tb) {
-    wait_staged();
-    int32_t t[32];
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int4 v = reinterpret_cast<const int4*>(lds + tb * kLdsBWords + q * 256)[lane];
-      t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
-    }
-    return precomp_from_words(t);
-  }
-  __device__ __forceinline__ void issue() {}
 };
 // B entries straight into registers, loaded late in the window (issue() runs
 // after the R entry's LDS pick, so the loads fly during the R addition): no
@@ -169,11 +112,6 @@ struct RegBTab {
 // edv_main_kernel_prio as a macro (text, not a function), so the plain kernel
 // compiles exactly as it did alone: an inlined-function form measured 2 %
 // slower at C2 (other register assignment; profiles/r04/ab_refactor_s11.jsonl).
-#ifndef EDV_MAIN_BLDS
-#define EDV_MAIN_BTAB RegBTab bt{a.btab, {0, 0}, {}};
-#else
-#define EDV_MAIN_BTAB LdsBTab bt{a.btab, wl + 2 * kLdsAWords, lane};
-#endif
 // (In the body: the digit loads are settled once, through opaque_i32, before
 // the window loop: the digit registers are shifted inside the loop, and the
 // waitcnt pass, merging the loop's back edge with loads still pending from the
@@ -209,17 +147,11 @@ _Pragma("unroll") \
   int32_t* wl = lds_main + (threadIdx.x >> 6) * kLdsWaveWords; \
   const int lane = int(threadIdx.x & 63); \
   LdsATab at{a.st.atab + j * kAWords, wl, lane}, rt{a.st.rtab + j * kAWords, wl + kLdsAWords, lane}; \
-  EDV_MAIN_BTAB \
-  MAIN_STAMP(1); \
-  a.accept[i] = main_one(da, db, bw, nwin, (wf >> 8) & 1, at, rt, bt) ? 1 : 0; \
-  MAIN_STAMP(15);
+  RegBTab bt{a.btab, {0, 0}, {}}; \
+  a.accept[i] = main_one(da, db, bw, nwin, (wf >> 8) & 1, at, rt, bt) ? 1 : 0;
 
 __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   __shared__ int32_t lds_main[(kBlock / 64) * kLdsWaveWords];
-#ifdef EDV_AB_SIDES  // prep-only measurement variant: the prep state is incomplete, so do nothing here
-  return;
-#endif
-  MAIN_STAMP(0);
   EDV_MAIN_BODY
 }
 
@@ -228,12 +160,10 @@ __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
 // (latency-bound SHA-512 chains) take the cycles it leaves, instead of
 // round-robin turns; in the plain paths the raised priority only costs (C2
 // sequential 0.698 against 0.678 ms, profiles/r04/ab_prio_s8.jsonl).
-#ifndef EDV_SPLIT_MAIN_PRIO
-#define EDV_SPLIT_MAIN_PRIO 2
-#endif
+constexpr int kSplitMainPrio = 2;
 __global__ __launch_bounds__(kBlock) void edv_main_kernel_prio(VerifyArgs a) {
   __shared__ int32_t lds_main[(kBlock / 64) * kLdsWaveWords];
-  __builtin_amdgcn_s_setprio(EDV_SPLIT_MAIN_PRIO);
+  __builtin_amdgcn_s_setprio(kSplitMainPrio);
   EDV_MAIN_BODY
 }
 
@@ -351,6 +281,17 @@ __global__ __launch_bounds__(kBlock) void edv_pack_bits_kernel(const uint8_t* ac
   bits[k] = uint8_t(b);
 }
 
+// Measurement helper of edv_profile_batch_dev_flush: read and rewrite a buffer
+// larger than the Infinity Cache, so whatever the previous kernel left there
+// (the prep kernel's tables) is evicted before the next one runs.
+__global__ __launch_bounds__(kBlock) void edv_flush_kernel(int4* p, uint64_t n16) {
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * kBlock) {
+    int4 v = p[i];
+    v.x += 1;
+    p[i] = v;
+  }
+}
+
 // j * B and j * 2^kBSplit B for j = 0..2^(kBBits-1) in affine precomp form, once per device
 __global__ void edv_btab_kernel(int32_t* out) {
   const int t = threadIdx.x + blockIdx.x * blockDim.x;
@@ -388,7 +329,7 @@ int set_err(int code, const char* what, hipError_t e = hipSuccess) {
 
 // HIP events of a measurement helper, destroyed on every return path
 struct Events {
-  hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
   int n = 0;
   int create(int k) {
     for (n = 0; n < k; n++) HIPOK(hipEventCreate(&e[n]), "event");
@@ -436,6 +377,10 @@ struct PinnedBuf {
 // fills every SIMD).  Sub-batch stream q uses scratch slots [q*P, (q+1)*P) of
 // the chunk state.
 constexpr int kQ = 4;
+// Message slices of the synchronous field-ordered path (run_shard_fields): the
+// hash side of slice k runs while slice k+1 copies.  edv_set_host_slices.
+constexpr int kSlices = 8;
+constexpr int kSlicesDefault = 4;
 // In-flight batches of the asynchronous host path per device: a Node keeps one
 // per prod in flight, and a pool of nodes in one process (C5) one per node, so
 // eight slots let up to eight callers overlap before a submission has to wait.
@@ -465,7 +410,7 @@ struct DevCtx {
   std::mutex mu;
   bool ready = false;
   std::atomic<bool> live{false};   // ready, readable without mu (placement, edv_context_count)
-  std::atomic<int> inflight{0};    // calls running here + async batches not yet completed
+  std::atomic<int> running{0};     // synchronous calls placed here and not yet returned
   int dev = -1;                    // logical device (edv_* device index)
   int phys = -1;                   // HIP device it runs on
   hipStream_t stream = nullptr;    // the library stream (edv_stream)
@@ -486,6 +431,8 @@ struct DevCtx {
   // split-prep host path (run_shard_split): copies on hcp, part q's prep on hs[q]
   hipStream_t hcp = nullptr;
   hipEvent_t part_copied[kQ] = {}, part_prepped[kQ] = {};
+  hipEvent_t slice_copied[kSlices] = {}, slice_hashed[kSlices] = {};
+  int host_slices = kSlicesDefault;
   // asynchronous host path (edv_verify_batch_async): kAsyncSlots slots used in turn,
   // H2D copies on hcp, kernels and the verdicts' D2H on hac, so the copies of
   // batch k+1 run while batch k computes
@@ -504,10 +451,9 @@ struct DevCtx {
   };
   AsyncSlot as[kAsyncSlots];
   hipStream_t hac = nullptr;
-  int64_t next_ticket = 0;
-  // tickets whose wait failed: their slot drops them (nothing is copied into the
-  // caller's buffers afterwards) and every later wait for them fails again
-  std::vector<int64_t> failed_tickets;
+  // tickets issued and failed (edv_ledger.h); a failed batch's slot drops it,
+  // so nothing is copied into the caller's buffers afterwards
+  AsyncLedger ledger;
   DevBuf sigs, pks, msgs, off, acc;
   PinnedBuf stage[kQ], acc_host;
   // Pipelined submission (edv_verify_batch_dev_pipelined): two state sets, a
@@ -566,6 +512,10 @@ int ctx_init(DevCtx& c) {
     if (!c.hs_end[q]) HIPOK(hipEventCreateWithFlags(&c.hs_end[q], hipEventDisableTiming), "event");
     if (!c.part_copied[q]) HIPOK(hipEventCreateWithFlags(&c.part_copied[q], hipEventDisableTiming), "event");
     if (!c.part_prepped[q]) HIPOK(hipEventCreateWithFlags(&c.part_prepped[q], hipEventDisableTiming), "event");
+  }
+  for (int k = 0; k < kSlices; k++) {
+    if (!c.slice_copied[k]) HIPOK(hipEventCreateWithFlags(&c.slice_copied[k], hipEventDisableTiming), "event");
+    if (!c.slice_hashed[k]) HIPOK(hipEventCreateWithFlags(&c.slice_hashed[k], hipEventDisableTiming), "event");
   }
   if (!c.hcp) HIPOK(hipStreamCreateWithFlags(&c.hcp, hipStreamNonBlocking), "hipStreamCreate");
   if (!c.hac) HIPOK(hipStreamCreateWithFlags(&c.hac, hipStreamNonBlocking), "hipStreamCreate");
@@ -695,8 +645,7 @@ uint32_t* bucket_ctr(ChunkBufs& b, int q) { return static_cast<uint32_t*>(b.buck
 // EDV_FLAG_BUCKETS forces them; otherwise the device mode decides
 // (edv_set_length_buckets).  Verdicts never depend on it.
 bool bucketing_enabled(const DevCtx& c, uint32_t flags) {
-  static const bool no_bucket = getenv("EDV_NO_BUCKET") != nullptr;  // A/B measurement knob
-  if (no_bucket || (flags & EDV_FLAG_UNIFORM_LENGTH)) return false;
+  if (flags & EDV_FLAG_UNIFORM_LENGTH) return false;
   if (flags & EDV_FLAG_BUCKETS) return true;
   return c.length_buckets != 0;
 }
@@ -890,24 +839,36 @@ void par_copy(const std::vector<Seg>& segs) {
   for (auto& x : th) x.join();
 }
 
-// memcpy of `bytes` into pinned staging, in K chunks over copy_threads()
-// threads, with chunk k's DMA to the device queued on stream s as soon as every
-// thread has copied its part of it, so the staging of chunk k+1 overlaps the
-// DMA of chunk k (pageable inputs of a synchronous call: the messages, 71 % of
-// a C2 batch's bytes).  Below 8 MiB: one par_copy, one DMA.
-int stage_and_send(uint8_t* dev, uint8_t* stage, const uint8_t* src, uint64_t bytes, hipStream_t s) {
+// memcpy of src[0, bounds[K]) into pinned staging over copy_threads() threads,
+// part by part (part k = [bounds[k], bounds[k+1])), with part k's DMA to the
+// device queued on stream s -- and ev[k], if given, recorded after it -- as
+// soon as every thread has copied its share of it, so the staging of part k+1
+// overlaps the DMA of part k (pageable inputs of a synchronous call: the
+// messages, 71 % of a C2 batch's bytes).  A copy below 8 MiB is staged by one
+// par_copy per part.
+int stage_and_send(uint8_t* dev, uint8_t* stage, const uint8_t* src, const uint64_t* bounds, int K, hipStream_t s,
+                   const hipEvent_t* ev) {
+  const uint64_t bytes = bounds[K] - bounds[0];
+  auto send = [&](int k) -> int {
+    const uint64_t c0 = bounds[k], c1 = bounds[k + 1];
+    if (c1 > c0) HIPOK(hipMemcpyAsync(dev + c0, stage + c0, c1 - c0, hipMemcpyHostToDevice, s), "h2d part");
+    if (ev) HIPOK(hipEventRecord(ev[k], s), "record");
+    return 0;
+  };
   if (bytes < (uint64_t(8) << 20)) {
-    par_copy({{stage, src, bytes}});
-    HIPOK(hipMemcpyAsync(dev, stage, bytes, hipMemcpyHostToDevice, s), "h2d");
+    int err;
+    for (int k = 0; k < K; k++) {
+      par_copy({{stage + bounds[k], src + bounds[k], bounds[k + 1] - bounds[k]}});
+      if ((err = send(k))) return err;
+    }
     return 0;
   }
-  constexpr int K = 4;
   const int T = copy_threads();
-  std::atomic<int> done[K];
+  std::vector<std::atomic<int>> done(K);
   for (auto& d : done) d.store(0);
   auto part = [&](int t) {
     for (int k = 0; k < K; k++) {
-      const uint64_t c0 = bytes * k / K, c1 = bytes * (k + 1) / K;
+      const uint64_t c0 = bounds[k], c1 = bounds[k + 1];
       const uint64_t a = c0 + (c1 - c0) * t / T, b = c0 + (c1 - c0) * (t + 1) / T;
       memcpy(stage + a, src + a, b - a);
       done[k].fetch_add(1, std::memory_order_release);
@@ -917,12 +878,10 @@ int stage_and_send(uint8_t* dev, uint8_t* stage, const uint8_t* src, uint64_t by
   for (int t = 1; t < T; t++) th.emplace_back(part, t);
   int err = 0;
   for (int k = 0; k < K; k++) {
-    const uint64_t c0 = bytes * k / K, c1 = bytes * (k + 1) / K;
-    const uint64_t a = c0, b = c0 + (c1 - c0) / T;
-    memcpy(stage + a, src + a, b - a);  // thread 0's part of chunk k
+    const uint64_t c0 = bounds[k], c1 = bounds[k + 1];
+    memcpy(stage + c0, src + c0, (c1 - c0) / T);  // thread 0's share of part k
     while (done[k].load(std::memory_order_acquire) < T - 1) std::this_thread::yield();
-    if (!err && hipMemcpyAsync(dev + c0, stage + c0, c1 - c0, hipMemcpyHostToDevice, s) != hipSuccess)
-      err = set_err(EDV_E_HIP, "h2d chunk");
+    if (!err) err = send(k);
   }
   for (auto& x : th) x.join();
   return err;
@@ -947,107 +906,38 @@ OffScan scan_offsets(const uint64_t* off, uint64_t lo, uint64_t hi) {
   return {bad == 0, diff == 0};
 }
 
-// Parts for the split-prep host path, 0 = not used.  A shard of one chunk
-// whose messages all have the same SHA-512 block count (no length buckets) is
-// copied in up to kQ parts; the prep of part q runs as soon as part q has
-// landed, on its own stream (a prep wave's latency, not the part's size, sets
-// its time, so the parts' preps run side by side), and one main kernel covers
-// the shard once every part is prepped (the main kernel also takes a whole
-// batch's time at any size, one wave per SIMD).  Measured at C2 (64k x 256 B,
-// profiles/r02/e2e_split_s31_s32.jsonl) it is within the box-to-box noise of the
-// one-sub-batch path (pinned 1.28-1.64 ms against 1.33-1.41 ms: the copy, 0.42
-// ms, is short next to the part's prep and the main kernel it still waits
-// for), so it is off unless EDV_HOST_PARTS (2..4) asks for it.
-int split_parts(const DevCtx& c, uint64_t n, bool varied) {
-  if (varied || n > c.chunk) return 0;
-  int p = 1;
-  if (const char* e = getenv("EDV_HOST_PARTS")) {
-    const int v = atoi(e);
-    if (v >= 1 && v <= kQ) p = v;
-  }
-  if (uint64_t(p) * 64 > n) p = 1;
-  return p > 1 ? p : 0;
-}
-
-// The split-prep host path (see split_parts) for requests [lo, hi) of a host
-// batch; device buffers sized by the caller, h_acc receives the verdicts.
-// Caller holds c.mu.
-int run_shard_split(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
-                    uint64_t lo, uint64_t hi, int parts, bool pinned, uint8_t* d_sigs, uint8_t* d_pks,
-                    uint8_t* d_msgs, uint64_t* d_off, uint8_t* d_acc, uint8_t* h_acc) {
-  const uint64_t n = hi - lo, mbase = off[lo];
-  // the scratch's previous users (any stream) finish before any prep writes it;
-  // the copy stream waits too, so a sequence of calls stays in order
-  HIPOK(hipStreamWaitEvent(c.hcp, c.st_done, 0), "wait scratch");
-  PinnedBuf& sl = c.stage[0];
-  uint8_t* p = nullptr;
-  if (!pinned) {
-    HIPOK(hipEventSynchronize(c.hs_staged[0]), "stage wait");  // the slot's previous H2D is done
-    if (sl.ensure(n * 96 + (n + parts) * 8 + (off[hi] - mbase))) return EDV_E_OOM;
-    p = static_cast<uint8_t*>(sl.p);
-  }
-  int err;
-  for (int q = 0; q < parts; q++) {
-    // part q: requests [a, b); its offsets get a private window of cnt + 1 at d_off + (a - lo) + q
-    const uint64_t a = lo + n * q / parts, b = lo + n * (q + 1) / parts, cnt = b - a;
-    const uint64_t mA = off[a], mB = off[b];
-    uint64_t* d_o = d_off + (a - lo) + q;
-    const uint8_t *src_s = sigs + 64 * a, *src_p = pks + 32 * a, *src_m = msgs + mA;
-    const uint8_t* src_o = reinterpret_cast<const uint8_t*>(off + a);
-    if (!pinned) {
-      // stage part q in the pinned slot (a parallel memcpy) while part q-1's H2D runs
-      uint8_t *ps = p + 64 * (a - lo), *pp = p + 64 * n + 32 * (a - lo), *po = p + 96 * n + 8 * ((a - lo) + q),
-              *pm = p + 96 * n + 8 * (n + parts) + (mA - mbase);
-      par_copy({{ps, src_s, 64 * cnt}, {pp, src_p, 32 * cnt}, {po, src_o, 8 * (cnt + 1)}, {pm, src_m, mB - mA}});
-      src_s = ps; src_p = pp; src_o = po; src_m = pm;
-    }
-    HIPOK(hipMemcpyAsync(d_sigs + 64 * (a - lo), src_s, cnt * 64, hipMemcpyHostToDevice, c.hcp), "h2d sigs");
-    HIPOK(hipMemcpyAsync(d_pks + 32 * (a - lo), src_p, cnt * 32, hipMemcpyHostToDevice, c.hcp), "h2d pks");
-    HIPOK(hipMemcpyAsync(d_o, src_o, (cnt + 1) * 8, hipMemcpyHostToDevice, c.hcp), "h2d off");
-    if (mB > mA) HIPOK(hipMemcpyAsync(d_msgs + (mA - mbase), src_m, mB - mA, hipMemcpyHostToDevice, c.hcp), "h2d msgs");
-    HIPOK(hipEventRecord(c.part_copied[q], c.hcp), "record");
-    hipStream_t s = c.hs[q];
-    HIPOK(hipStreamWaitEvent(s, c.part_copied[q], 0), "wait copy");
-    // slots [a - lo, b - lo) of the chunk scratch, so the main kernel sees the shard as one chunk
-    VerifyArgs va = make_args(c, c.st, d_sigs + 64 * (a - lo), d_pks + 32 * (a - lo), d_msgs, d_o, mbase,
-                              d_acc + (a - lo), false, a - lo);
-    va.n = cnt;
-    if ((err = launch_prep(bucket_ctr(c.st, q), va, d_o, false, s))) return err;
-    HIPOK(hipEventRecord(c.part_prepped[q], s), "record");
-  }
-  if (!pinned) HIPOK(hipEventRecord(c.hs_staged[0], c.hcp), "record");
-  hipStream_t s0 = c.hs[0];
-  for (int q = 1; q < parts; q++) HIPOK(hipStreamWaitEvent(s0, c.part_prepped[q], 0), "wait prep");
-  VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, mbase, d_acc, false, 0);
-  va.n = n;
-  if ((err = launch_main(va, s0))) return err;
-  HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, s0), "d2h accept");
-  HIPOK(hipEventRecord(c.st_done, s0), "record scratch");
-  HIPOK(hipStreamWaitEvent(c.stream, c.st_done, 0), "join");
-  HIPOK(hipStreamSynchronize(s0), "stream sync");
-  return 0;
-}
-
 // A shard of one chunk, copied field by field (the default host path for a
 // shard that fits one chunk).  Splitting the copy by requests cannot help: a
 // sub-batch's kernels take a whole batch's time (latency-bound lanes, DESIGN.md
 // section 3).  Splitting it by input field can: the two point sides need only
 // the signatures (R) and keys (A), 27 % of the bytes, and the hash side only
-// runs after the messages (71 %) land.  So: H2D of sigs, pks and offsets, then
-// of the messages, on the copy stream; the point sides (and the length buckets)
-// start on stream hs[0] as soon as the first part is in, while the messages
-// still copy; the hash side on hs[1] once they are in; the main kernel on hs[0]
-// after both; then the verdicts' D2H.  Caller holds c.mu.
+// the messages (71 %) besides.  So: H2D of sigs, pks and offsets, then of the
+// messages in `slices` slices by request, on the copy stream; the point sides
+// (and the length buckets) start on stream hs[0] as soon as the first part is
+// in, while the messages still copy; the hash side of each slice on hs[1..3]
+// (in turn) as soon as its messages are in, so only the last slice's hash side
+// is left after the copy; the main kernel on hs[0] after all of them; then the
+// verdicts' D2H.  Length-bucketed shards (messages of several SHA-512 block
+// counts) hash in one piece after the whole copy: the bucket permutation
+// spans the shard.  Caller holds c.mu.
 int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
                      uint64_t lo, uint64_t hi, bool pinned, bool varied, uint8_t* d_sigs, uint8_t* d_pks,
                      uint8_t* d_msgs, uint64_t* d_off, uint8_t* d_acc, uint8_t* h_acc) {
   const uint64_t n = hi - lo, mbase = off[lo], mbytes = off[hi] - mbase;
-  const hipStream_t cp = c.hcp, s0 = c.hs[0], s1 = c.hs[1];
+  const hipStream_t cp = c.hcp, s0 = c.hs[0];
+  const bool bucket = bucketing_enabled(c, varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH);
+  // slices of whole workgroups (256 requests), at most kSlices
+  int K = bucket ? 1 : c.host_slices;
+  if (uint64_t(K) * kBlock > n) K = int(n / kBlock) > 1 ? int(n / kBlock) : 1;
+  uint64_t rb[kSlices + 1], mb[kSlices + 1];  // request / message-byte bounds of the slices (shard-relative)
+  for (int k = 0; k <= K; k++) {
+    rb[k] = k == K ? n : (n * k / K) / kBlock * kBlock;
+    mb[k] = off[lo + rb[k]] - mbase;
+  }
   // the scratch's previous users (any stream) finish before the kernels write it,
   // and the copies follow the previous call's
   HIPOK(hipStreamWaitEvent(cp, c.st_done, 0), "wait scratch");
-  HIPOK(hipStreamWaitEvent(s0, c.st_done, 0), "wait scratch");
-  HIPOK(hipStreamWaitEvent(s1, c.st_done, 0), "wait scratch");
+  for (int q = 0; q < kQ; q++) HIPOK(hipStreamWaitEvent(c.hs[q], c.st_done, 0), "wait scratch");
   const uint8_t *src_s = sigs + 64 * lo, *src_p = pks + 32 * lo, *src_m = msgs + mbase;
   const uint8_t* src_o = reinterpret_cast<const uint8_t*>(off + lo);
   PinnedBuf& sl = c.stage[0];
@@ -1063,33 +953,45 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
   HIPOK(hipMemcpyAsync(d_off, src_o, (n + 1) * 8, hipMemcpyHostToDevice, cp), "h2d off");
   HIPOK(hipEventRecord(c.part_copied[0], cp), "record");
   int err;
-  if (!pinned) {
-    // stage the messages while the first part's DMA and the point sides run,
-    // each quarter's DMA queued as soon as it is staged
-    uint8_t* pm = static_cast<uint8_t*>(sl.p) + 96 * n + 8 * (n + 1);
-    if (mbytes && (err = stage_and_send(d_msgs, pm, src_m, mbytes, cp))) return err;
-  } else if (mbytes) {
-    HIPOK(hipMemcpyAsync(d_msgs, src_m, mbytes, hipMemcpyHostToDevice, cp), "h2d msgs");
-  }
-  HIPOK(hipEventRecord(c.part_copied[1], cp), "record");
-  if (!pinned) HIPOK(hipEventRecord(c.hs_staged[0], cp), "record");
-  const bool bucket = bucketing_enabled(c, varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH);
+  // the point sides first: they need only what has just been queued
   VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, mbase, d_acc, bucket);
   va.n = n;
   HIPOK(hipStreamWaitEvent(s0, c.part_copied[0], 0), "wait copy");
   if (bucket && (err = launch_buckets(bucket_ctr(c.st, 0), va, d_off, s0))) return err;
   HIPOK(hipEventRecord(c.part_prepped[0], s0), "record");  // the bucket permutation is written
-  VerifyArgs vp = va, vh = va;
+  VerifyArgs vp = va;
   vp.side0 = 1;
   vp.nsides = 2;
-  vh.side0 = 0;
-  vh.nsides = 1;
   if ((err = launch_prep_sides(vp, s0))) return err;
-  HIPOK(hipStreamWaitEvent(s1, c.part_copied[1], 0), "wait copy");
-  HIPOK(hipStreamWaitEvent(s1, c.part_prepped[0], 0), "wait buckets");
-  if ((err = launch_prep_sides(vh, s1))) return err;
-  HIPOK(hipEventRecord(c.part_prepped[1], s1), "record");
-  HIPOK(hipStreamWaitEvent(s0, c.part_prepped[1], 0), "wait hash side");
+  // then the messages, slice by slice (staged in the same slices when pageable)
+  if (!pinned) {
+    uint8_t* pm = static_cast<uint8_t*>(sl.p) + 96 * n + 8 * (n + 1);
+    if (mbytes && (err = stage_and_send(d_msgs, pm, src_m, mb, K, cp, c.slice_copied))) return err;
+    if (!mbytes)
+      for (int k = 0; k < K; k++) HIPOK(hipEventRecord(c.slice_copied[k], cp), "record");
+    HIPOK(hipEventRecord(c.hs_staged[0], cp), "record");
+  } else {
+    for (int k = 0; k < K; k++) {
+      if (mb[k + 1] > mb[k])
+        HIPOK(hipMemcpyAsync(d_msgs + mb[k], src_m + mb[k], mb[k + 1] - mb[k], hipMemcpyHostToDevice, cp), "h2d msgs");
+      HIPOK(hipEventRecord(c.slice_copied[k], cp), "record");
+    }
+  }
+  for (int k = 0; k < K; k++) {
+    const hipStream_t hk = c.hs[1 + k % (kQ - 1)];
+    // requests [rb[k], rb[k+1]) of the shard: scratch slots and request index
+    // both start at rb[k] (a bucketed shard is one slice, over the permutation)
+    VerifyArgs vh = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, mbase, d_acc, bucket, rb[k]);
+    vh.base = rb[k];
+    vh.n = rb[k + 1] - rb[k];
+    vh.side0 = 0;
+    vh.nsides = 1;
+    HIPOK(hipStreamWaitEvent(hk, c.slice_copied[k], 0), "wait copy");
+    if (bucket) HIPOK(hipStreamWaitEvent(hk, c.part_prepped[0], 0), "wait buckets");
+    if ((err = launch_prep_sides(vh, hk))) return err;
+    HIPOK(hipEventRecord(c.slice_hashed[k], hk), "record");
+  }
+  for (int k = 0; k < K; k++) HIPOK(hipStreamWaitEvent(s0, c.slice_hashed[k], 0), "wait hash side");
   if ((err = launch_main(va, s0))) return err;
   HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, s0), "d2h accept");
   HIPOK(hipEventRecord(c.st_done, s0), "record scratch");
@@ -1113,11 +1015,7 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
   // batch's latency at one wave per SIMD.  A larger shard alternates two
   // streams of half-chunk sub-batches, so the H2D copy of one overlaps the
   // kernels of the other.  EDV_HOST_STREAMS (1..4) overrides, for measurement.
-  int Q = (n > c.chunk && c.chunk >= 2 * uint64_t(kBlock)) ? 2 : 1;
-  if (const char* e = getenv("EDV_HOST_STREAMS")) {
-    const int v = atoi(e);
-    if (v >= 1 && v <= kQ && c.chunk >= uint64_t(v) * kBlock) Q = v;
-  }
+  const int Q = (n > c.chunk && c.chunk >= 2 * uint64_t(kBlock)) ? 2 : 1;
   const uint64_t pmax = c.chunk / Q;
   uint64_t P = (n + Q - 1) / Q;
   P = ((P + 63) / 64) * 64;
@@ -1141,20 +1039,9 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
   uint8_t* d_acc = static_cast<uint8_t*>(c.acc.p);
   uint8_t* h_acc = acc_pinned ? accept + lo : static_cast<uint8_t*>(c.acc_host.p);
   int err;
-  // One chunk of fixed-length requests: copy in parts, prep each part as it
-  // lands, one main kernel over the whole shard.
-  if (const int parts = split_parts(c, n, varied)) {
-    if (c.off.ensure((n + parts) * 8)) return EDV_E_OOM;
-    if ((err = run_shard_split(c, sigs, pks, msgs, off, lo, hi, parts, pinned, d_sigs, d_pks, d_msgs,
-                               static_cast<uint64_t*>(c.off.p), d_acc, h_acc)))
-      return err;
-    if (!acc_pinned) memcpy(accept + lo, h_acc, n);
-    return 0;
-  }
   // One chunk: copied field by field, the point sides starting before the
-  // messages are in (EDV_HOST_FIELDS=0 restores the one-sub-batch path for A/B).
-  const char* fe = getenv("EDV_HOST_FIELDS");
-  if (nsub == 1 && !(fe && atoi(fe) == 0)) {
+  // messages are in.
+  if (nsub == 1) {
     if ((err = run_shard_fields(c, sigs, pks, msgs, off, lo, hi, pinned, varied, d_sigs, d_pks, d_msgs, d_off,
                                 d_acc, h_acc)))
       return err;
@@ -1174,31 +1061,20 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
     const uint64_t* src_o = off + a;
     if (!pinned) {
       // pageable: staged through this stream's pinned slot (a parallel memcpy),
-      // then copied by DMA.  Staging in four parts with each part's H2D queued as
-      // soon as it was staged measured slower at C2 (2.43 vs 1.78 ms per 64k:
-      // profiles/r02/e2e_probe_s6.json), the sixteen small copies costing more
-      // than the overlap saved.
+      // then copied by DMA.  (Staging in four parts with each part's H2D queued
+      // as soon as it was staged measured slower at C2, 2.43 vs 1.78 ms per 64k:
+      // profiles/r02/e2e_probe_s6.json.)
       PinnedBuf& sl = c.stage[q];
       HIPOK(hipEventSynchronize(c.hs_staged[q]), "stage wait");  // the slot's previous H2D is done
       if (sl.ensure(cnt * 96 + (cnt + 1) * 8 + (mB - mA))) return EDV_E_OOM;
       uint8_t* p = static_cast<uint8_t*>(sl.p);
       uint8_t *ps = p, *pp = p + cnt * 64, *po = p + cnt * 96, *pm = p + cnt * 96 + (cnt + 1) * 8;
-      const uint64_t bytes = cnt * 104 + (mB - mA);
-      const uint64_t parts = getenv("EDV_STAGE_PARTS") && bytes >= (uint64_t(8) << 20) && cnt >= 4 ? 4 : 1;
-      for (uint64_t j = 0; j < parts; j++) {
-        const uint64_t r0 = cnt * j / parts, r1 = cnt * (j + 1) / parts;  // requests [a + r0, a + r1)
-        const uint64_t m0 = off[a + r0] - mA, m1 = off[a + r1] - mA;
-        par_copy({{ps + 64 * r0, src_s + 64 * r0, 64 * (r1 - r0)}, {pp + 32 * r0, src_p + 32 * r0, 32 * (r1 - r0)},
-                  {po + 8 * r0, reinterpret_cast<const uint8_t*>(src_o + r0), 8 * (r1 - r0 + 1)},
-                  {pm + m0, src_m + m0, m1 - m0}});
-        HIPOK(hipMemcpyAsync(d_sigs + 64 * (a - lo + r0), ps + 64 * r0, 64 * (r1 - r0), hipMemcpyHostToDevice, s),
-              "h2d sigs");
-        HIPOK(hipMemcpyAsync(d_pks + 32 * (a - lo + r0), pp + 32 * r0, 32 * (r1 - r0), hipMemcpyHostToDevice, s),
-              "h2d pks");
-        HIPOK(hipMemcpyAsync(d_o + r0, po + 8 * r0, 8 * (r1 - r0 + 1), hipMemcpyHostToDevice, s), "h2d off");
-        if (m1 > m0)
-          HIPOK(hipMemcpyAsync(d_msgs + (mA - mbase) + m0, pm + m0, m1 - m0, hipMemcpyHostToDevice, s), "h2d msgs");
-      }
+      par_copy({{ps, src_s, 64 * cnt}, {pp, src_p, 32 * cnt}, {po, reinterpret_cast<const uint8_t*>(src_o), 8 * (cnt + 1)},
+                {pm, src_m, mB - mA}});
+      HIPOK(hipMemcpyAsync(d_sigs + 64 * (a - lo), ps, 64 * cnt, hipMemcpyHostToDevice, s), "h2d sigs");
+      HIPOK(hipMemcpyAsync(d_pks + 32 * (a - lo), pp, 32 * cnt, hipMemcpyHostToDevice, s), "h2d pks");
+      HIPOK(hipMemcpyAsync(d_o, po, 8 * (cnt + 1), hipMemcpyHostToDevice, s), "h2d off");
+      if (mB > mA) HIPOK(hipMemcpyAsync(d_msgs + (mA - mbase), pm, mB - mA, hipMemcpyHostToDevice, s), "h2d msgs");
     } else {
       HIPOK(hipMemcpyAsync(d_sigs + 64 * (a - lo), src_s, cnt * 64, hipMemcpyHostToDevice, s), "h2d sigs");
       HIPOK(hipMemcpyAsync(d_pks + 32 * (a - lo), src_p, cnt * 32, hipMemcpyHostToDevice, s), "h2d pks");
@@ -1254,15 +1130,8 @@ int run_digest_shard(DevCtx& c, const uint8_t* msgs, const uint64_t* off, uint64
 
 // Asynchronous host path.  Wait for a slot's batch and hand over its verdicts.
 void async_fail(DevCtx& c, DevCtx::AsyncSlot& s) {
-  if (c.failed_tickets.size() >= 256) c.failed_tickets.erase(c.failed_tickets.begin());
-  c.failed_tickets.push_back(s.ticket);
+  c.ledger.fail(s.ticket);
   s.ticket = -1;
-  c.inflight.fetch_sub(1);
-}
-bool ticket_failed(const DevCtx& c, int64_t t) {
-  for (int64_t x : c.failed_tickets)
-    if (x == t) return true;
-  return false;
 }
 int async_complete(DevCtx& c, DevCtx::AsyncSlot& s) {
   if (s.ticket < 0) return 0;
@@ -1273,7 +1142,6 @@ int async_complete(DevCtx& c, DevCtx::AsyncSlot& s) {
   if (!s.acc_pinned) memcpy(s.accept, s.acc_host.p, s.n);
   if (s.digests && !s.dig_pinned) memcpy(s.digests, s.dig_host.p, 32 * s.n);
   s.ticket = -1;
-  c.inflight.fetch_sub(1);
   return 0;
 }
 
@@ -1285,10 +1153,13 @@ int async_complete(DevCtx& c, DevCtx::AsyncSlot& s) {
 // submissions later, after its batch is complete.  Caller holds c.mu.
 int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
                  uint64_t n, uint8_t* accept, uint8_t* digests, int64_t* ticket) {
-  const int64_t t = c.next_ticket;
+  const int64_t t = c.ledger.next;
   DevCtx::AsyncSlot& s = c.as[t % kAsyncSlots];
   int err;
   if ((err = async_complete(c, s))) return err;  // the batch of kAsyncSlots submissions ago
+  // an unfilled verdict buffer rejects: whatever happens to this batch, no stale
+  // byte of a reused buffer can read as "accept"
+  memset(accept, 0, n);
   const uint64_t mbase = off[0], mbytes = off[n] - mbase;
   if (s.sigs.ensure(n * 64) || s.pks.ensure(n * 32) || s.msgs.ensure(mbytes + 64) || s.off.ensure((n + 1) * 8) ||
       s.acc.ensure(n) || (digests && s.dig.ensure(32 * n)))
@@ -1343,13 +1214,11 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
     HIPOK(hipMemcpyAsync(h_dig, d_dig, 32 * n, hipMemcpyDeviceToHost, ks), "d2h digests");
   }
   HIPOK(hipEventRecord(s.done, ks), "record");
-  c.inflight.fetch_add(1);
   s.ticket = t;
   s.accept = accept;
   s.digests = digests;
   s.n = n;
-  c.next_ticket = t + 1;
-  *ticket = t;
+  *ticket = c.ledger.issue();
   return 0;
 }
 
@@ -1403,31 +1272,75 @@ uint64_t min_shard() {
   return v;
 }
 
-// The device for a batch that runs on one device, among `devs`: an initialised
-// device with nothing in flight (the lowest-loaded initialised one first, so a
-// process that verifies one batch at a time stays on one context); if every
-// initialised device is busy, a device not yet initialised (in an order that
-// starts at pid mod ndev, so the processes of a node spread over its GPUs);
-// else the least-loaded device.
-int pick_device(const std::vector<int>& devs) {
-  const int k = int(devs.size());
-  if (k == 1) return devs[0];
-  const int start = int(uint64_t(getpid()) % uint64_t(k));
-  int best = -1, best_load = 0;
-  for (int j = 0; j < k; j++) {
-    const int d = devs[(start + j) % k];
-    if (!g_ctx[d]->live.load()) continue;
-    const int load = g_ctx[d]->inflight.load();
-    if (best < 0 || load < best_load) { best = d; best_load = load; }
-  }
-  if (best >= 0 && best_load == 0) return best;
-  for (int j = 0; j < k; j++) {
-    const int d = devs[(start + j) % k];
-    if (!g_ctx[d]->live.load()) return d;
-  }
-  if (best >= 0) return best;
-  return devs[start];
+// Asynchronous batches of a context still running on the GPU: slots holding a
+// ticket whose done event has not completed (a batch stops counting as soon as
+// it is finished, waited for or not).  If another thread holds the context's
+// lock, a call is running there: count it as one.
+int async_running(DevCtx& c) {
+  std::unique_lock<std::mutex> lk(c.mu, std::try_to_lock);
+  if (!lk.owns_lock()) return 1;
+  int k = 0;
+  for (auto& s : c.as)
+    if (s.ticket >= 0 && s.done && hipEventQuery(s.done) == hipErrorNotReady) k++;
+  (void)hipGetLastError();  // hipErrorNotReady is not an error of ours
+  return k;
 }
+int device_load(int d) {
+  DevCtx& c = *g_ctx[d];
+  return c.running.load() + (c.live.load() ? async_running(c) : 0);
+}
+
+// Placement of the g shards of a batch on g of the devices `devs` (g == 1: a
+// batch that runs on one device).  Preference: initialised devices with nothing
+// running (so a process that verifies one batch at a time stays on its
+// contexts); then devices not yet initialised, in an order that starts at pid
+// mod ndev (the processes of a node spread over its GPUs); then the least-loaded
+// busy devices.  Load = synchronous calls placed on the device + its asynchronous
+// batches still running.  Chosen devices are reserved (running + 1) under one
+// placement lock, so concurrent callers see each other's choices; the caller
+// releases them (Placed).
+std::mutex g_place_mu;
+std::vector<int> place(const std::vector<int>& devs, uint32_t g) {
+  const int k = int(devs.size());
+  std::vector<int> out;
+  std::lock_guard<std::mutex> lk(g_place_mu);
+  if (uint32_t(k) <= g) {
+    out = devs;
+  } else {
+    const int start = int(uint64_t(getpid()) % uint64_t(k));
+    std::vector<std::pair<int, int>> busy;  // (load, device)
+    std::vector<int> idle, fresh;
+    for (int j = 0; j < k; j++) {
+      const int d = devs[(start + j) % k];
+      if (!g_ctx[d]->live.load()) {
+        if (g_ctx[d]->running.load()) busy.push_back({g_ctx[d]->running.load(), d});  // being initialised
+        else fresh.push_back(d);
+        continue;
+      }
+      const int load = device_load(d);
+      if (load == 0) idle.push_back(d);
+      else busy.push_back({load, d});
+    }
+    std::stable_sort(busy.begin(), busy.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    for (int d : idle) out.push_back(d);
+    for (int d : fresh) out.push_back(d);
+    for (auto& b : busy) out.push_back(b.second);
+    out.resize(g);
+  }
+  for (int d : out) g_ctx[d]->running.fetch_add(1);
+  return out;
+}
+int pick_device(const std::vector<int>& devs) {
+  if (devs.size() == 1) return devs[0];
+  const int d = place(devs, 1)[0];
+  g_ctx[d]->running.fetch_sub(1);  // a pick only advises (edv_pick_device): no reservation kept
+  return d;
+}
+// Releases a device reserved by place() when the shard on it returns.
+struct Placed {
+  DevCtx* c;
+  ~Placed() { c->running.fetch_sub(1); }
+};
 
 std::vector<int> devices_of(uint32_t device_mask, int* err) {
   int ndev;
@@ -1442,17 +1355,10 @@ std::vector<int> devices_of(uint32_t device_mask, int* err) {
   return devs;
 }
 
-// Counts a call as in flight on its device while it runs.
-struct Inflight {
-  DevCtx* c;
-  explicit Inflight(DevCtx* x) : c(x) { c->inflight.fetch_add(1); }
-  ~Inflight() { c->inflight.fetch_sub(1); }
-};
-
 // Validate a host batch and split [0, n) over the devices of device_mask (at
 // most one shard per min_shard() requests), one host thread per shard; a batch
-// that is one shard runs on the calling thread on pick_device's device.
-// shard(ctx, lo, hi) does the work under the context lock.
+// that is one shard runs on the calling thread.  The devices are place()'s
+// choice.  shard(ctx, lo, hi) does the work under the context lock.
 template <class Shard>
 int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard shard) {
   int err;
@@ -1460,16 +1366,16 @@ int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard 
   if (err) return err;
   const uint64_t most = n / min_shard();
   const uint32_t g = uint32_t(most < devs.size() ? (most > 1 ? most : 1) : devs.size());
+  const std::vector<int> on = place(devs, g);
   auto one = [&](int dev, uint64_t lo, uint64_t hi) {
-    Inflight inf(g_ctx[dev]);
+    Placed placed{g_ctx[dev]};
     CtxLock cl(dev);
     if (cl.err) return cl.err;
     const int rc = shard(*cl.c, lo, hi);
     if (rc) quiesce(*cl.c);
     return rc;
   };
-  if (g == 1) return one(pick_device(devs), 0, n);
-  devs.resize(g);
+  if (g == 1) return one(on[0], 0, n);
   std::vector<uint64_t> bounds(g + 1);
   shard_bounds(off, n, g, bounds.data());
   std::vector<int> rc(g, 0);
@@ -1477,7 +1383,7 @@ int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard 
   std::vector<std::thread> th;
   for (uint32_t k = 0; k < g; k++) {
     th.emplace_back([&, k]() {
-      rc[k] = one(devs[k], bounds[k], bounds[k + 1]);
+      rc[k] = one(on[k], bounds[k], bounds[k + 1]);
       errs[k] = g_err;
     });
   }
@@ -1509,8 +1415,6 @@ extern "C" {
 // edv.lib() refuses them unless EDV_ALLOW_MEASUREMENT_LIB=1.
 #if defined(EDV_MEASURE_NO_VERIFY)
 const char* edv_version(void) { return "edv 0.2.0 gfx950 MEASUREMENT-ONLY: verification skipped"; }
-#elif defined(EDV_AB_SIDES)
-const char* edv_version(void) { return "edv 0.2.0 gfx950 MEASUREMENT-ONLY: prep sides subset, wrong verdicts"; }
 #else
 const char* edv_version(void) { return "edv 0.2.0 gfx950"; }
 #endif
@@ -1554,6 +1458,7 @@ int edv_verify_batch(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msg
   if (!msgs && msg_off[n] != msg_off[0]) return set_err(EDV_E_ARG, "null msgs");
   int err;
   if ((err = check_offsets(msg_off, n))) return err;
+  memset(accept, 0, n);  // fail closed: a call that fails part-way leaves rejections
   return for_each_shard(msg_off, n, device_mask, [&](DevCtx& c, uint64_t lo, uint64_t hi) {
     return run_shard(c, sigs, pks, msgs, msg_off, lo, hi, accept);
   });
@@ -1576,7 +1481,7 @@ int edv_verify_digest_batch_async(const uint8_t* sigs, const uint8_t* pks, const
   CtxLock cl(device);
   if (cl.err) return cl.err;
   if (n == 0) {
-    *ticket = cl.c->next_ticket++;
+    *ticket = cl.c->ledger.issue();
     return 0;
   }
   if ((err = submit_async(*cl.c, sigs, pks, msgs, msg_off, n, accept, digests, ticket))) {
@@ -1595,8 +1500,7 @@ int edv_wait_async(int device, int64_t ticket) {
   g_err.clear();
   CtxLock cl(device);
   if (cl.err) return cl.err;
-  if (ticket < 0 || ticket >= cl.c->next_ticket) return set_err(EDV_E_ARG, "unknown ticket");
-  if (ticket_failed(*cl.c, ticket)) return set_err(EDV_E_HIP, "async batch failed earlier");
+  if (!cl.c->ledger.known(ticket)) return set_err(EDV_E_ARG, "unknown ticket");
   for (auto& s : cl.c->as) {
     if (s.ticket != ticket) continue;
     // wait without holding the device lock (other threads keep submitting);
@@ -1611,8 +1515,9 @@ int edv_wait_async(int device, int64_t ticket) {
     }
     return s.ticket == ticket ? async_complete(*cl.c, s) : 0;
   }
-  // already complete (waited for, or its slot was reused) -- unless it failed meanwhile
-  if (ticket_failed(*cl.c, ticket)) return set_err(EDV_E_HIP, "async batch failed earlier");
+  // already complete (waited for, or its slot was reused) -- unless a batch at
+  // or after it failed (sticky, edv_ledger.h)
+  if (cl.c->ledger.settled(ticket) != 0) return set_err(EDV_E_HIP, "async batch failed earlier");
   return 0;
 }
 
@@ -1634,7 +1539,15 @@ int edv_pack_bits_dev(const uint8_t* d_accept, uint64_t n, uint8_t* d_bits, int 
   if (!d_accept || !d_bits) return set_err(EDV_E_ARG, "null pointer");
   CtxLock cl(device);
   if (cl.err) return cl.err;
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : cl.c->stream;
+  DevCtx* c = cl.c;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  // after every verify launched on this device so far, on whatever stream:
+  // the ordinary paths record st_done after their last kernel, the pipelined
+  // path main_done per state set
+  HIPOK(hipStreamWaitEvent(s, c->st_done, 0), "wait verdicts");
+  if (c->pipe_ready)
+    for (int b = 0; b < 2; b++)
+      if (c->pending[b]) HIPOK(hipStreamWaitEvent(s, c->main_done[b], 0), "wait verdicts");
   const uint64_t nb = (n + 7) / 8;
   edv_pack_bits_kernel<<<dim3(unsigned((nb + kBlock - 1) / kBlock)), dim3(kBlock), 0, s>>>(d_accept, n, d_bits);
   HIPOK(hipGetLastError(), "pack bits launch");
@@ -1789,6 +1702,17 @@ int edv_set_chunk(int device, uint64_t chunk) {
   return 0;
 }
 
+int edv_set_host_slices(int device, int slices) {
+  g_err.clear();
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  if (slices < 0 || slices > kSlices) return set_err(EDV_E_ARG, "slices must be 0..8");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->host_slices = slices ? slices : kSlicesDefault;
+  return 0;
+}
+
 int edv_set_length_buckets(int device, int mode) {
   g_err.clear();
   int err = 0;
@@ -1800,9 +1724,10 @@ int edv_set_length_buckets(int device, int mode) {
   return 0;
 }
 
-int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
-                          const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, int device,
-                          int iters, float* ms_prep, float* ms_main) {
+int edv_profile_batch_dev_flush(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
+                                const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept,
+                                int device, int iters, uint64_t flush_bytes, float* ms_prep, float* ms_flush,
+                                float* ms_main) {
   g_err.clear();
   int err;
   if ((err = check_dev_align(d_sigs, d_pks, d_msg_off))) return err;
@@ -1815,10 +1740,14 @@ int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uin
   va.n = n;
   uint32_t* hist = bucket_ctr(c->st, 0);
   const unsigned blocks = unsigned((n + kBlock - 1) / kBlock);
+  DevBuf flush;
+  flush_bytes &= ~uint64_t(15);
+  if (flush_bytes && flush.ensure(flush_bytes)) return EDV_E_OOM;
+  if (flush_bytes) HIPOK(hipMemsetAsync(flush.p, 0, flush_bytes, c->stream), "memset flush");
   Events ev;
-  if ((err = ev.create(3))) return err;
+  if ((err = ev.create(4))) return err;
   HIPOK(hipStreamWaitEvent(c->stream, c->st_done, 0), "wait scratch");
-  float tp = 0, tm = 0;
+  float tp = 0, tf = 0, tm = 0;
   for (int it = 0; it < iters; it++) {
     if (bucket) {
       HIPOK(hipMemsetAsync(hist, 0, 2 * kBuckets * 4, c->stream), "memset buckets");
@@ -1829,19 +1758,33 @@ int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uin
     HIPOK(hipEventRecord(ev.e[0], c->stream), "record");
     HIPOK(launch_prep_kernel(3 * blocks, c->stream, va), "prep launch");
     HIPOK(hipEventRecord(ev.e[1], c->stream), "record");
-    edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(va);
+    if (flush_bytes)
+      edv_flush_kernel<<<dim3(4096), dim3(kBlock), 0, c->stream>>>(static_cast<int4*>(flush.p), flush_bytes / 16);
     HIPOK(hipEventRecord(ev.e[2], c->stream), "record");
-    HIPOK(hipEventSynchronize(ev.e[2]), "event sync");
-    float a = 0, b = 0;
+    edv_main_kernel<<<dim3(blocks), dim3(kBlock), 0, c->stream>>>(va);
+    HIPOK(hipEventRecord(ev.e[3], c->stream), "record");
+    HIPOK(hipEventSynchronize(ev.e[3]), "event sync");
+    float a = 0, b = 0, m = 0;
     HIPOK(hipEventElapsedTime(&a, ev.e[0], ev.e[1]), "elapsed");
     HIPOK(hipEventElapsedTime(&b, ev.e[1], ev.e[2]), "elapsed");
+    HIPOK(hipEventElapsedTime(&m, ev.e[2], ev.e[3]), "elapsed");
     tp += a;
-    tm += b;
+    tf += b;
+    tm += m;
   }
   HIPOK(hipEventRecord(c->st_done, c->stream), "record scratch");
+  HIPOK(hipStreamSynchronize(c->stream), "stream sync");  // the flush buffer is freed on return
   if (ms_prep) *ms_prep = tp / iters;
+  if (ms_flush) *ms_flush = tf / iters;
   if (ms_main) *ms_main = tm / iters;
   return 0;
+}
+
+int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
+                          const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, int device,
+                          int iters, float* ms_prep, float* ms_main) {
+  return edv_profile_batch_dev_flush(d_sigs, d_pks, d_msgs, d_msg_off, msg_base, n, d_accept, device, iters, 0,
+                                     ms_prep, nullptr, ms_main);
 }
 
 int edv_dev_alloc(int device, uint64_t bytes, void** out) {

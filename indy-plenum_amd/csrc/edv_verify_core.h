@@ -31,31 +31,19 @@ namespace edv {
 // [b S mod L]B = [s_lo]B + [s_hi](2^126 B): 8 signed radix-2^16 digits of each
 // half against shared tables 0..2^15 x B and 0..2^15 x 2^126 B (4 MiB each),
 // both added at every fourth window (16 = 4 x 4 bits) from window 28 down.
-// EDV_AWIN=5 builds the earlier layout for A/B runs: 5-bit windows, 17-entry
-// tables, ~27 windows; radix-2^15 B digits split at 2^130, every third window
-// from window 24.  Measured: 4-bit windows make the prep kernel 17 % faster
-// (half the table) and the main kernel 3 % slower (more additions), net +5 %
-// (profiles/r02/ab_w4_s43.jsonl).
-#ifndef EDV_AWIN
-#define EDV_AWIN 4
-#endif
-// Phase stamps of the diagnostic build (EDV_STAMPS, tools/stamps.py): a no-op
-// everywhere else, the real kernels and the CPU build included.
-#ifndef EDV_STAMP
-#define EDV_STAMP(slot) ((void)0)
-#endif
-static_assert(EDV_AWIN == 4 || EDV_AWIN == 5, "window width 4 or 5");
-constexpr int kAWin = EDV_AWIN;                 // bits per [a](-A) / [b](-R) window
-constexpr int kAWindows = (255 + kAWin - 1) / kAWin;  // at most: 64 x 4 = 256 (51 x 5 = 255) bits >= 253
-constexpr int kAEntries = (1 << (kAWin - 1)) + 1;     // per-lane table 0..8 (0..16) x P, cached form (entry 0 = identity)
-constexpr int kBBits = kAWin == 5 ? 15 : 16;    // radix 2^16 (2^15) digits of the B scalar halves
-constexpr int kBSplit = kAWin == 5 ? 130 : 126; // s = s_lo + 2^126 s_hi (2^130)
-// digits per half: 8 x 16 = 128 bits for s_lo < 2^126 and s_hi < 2^127 (9 x 15 = 135 >= 131); s_hi's top
+// (5-bit windows -- 17-entry tables, ~27 windows -- made the prep kernel 17 %
+// slower for a main kernel 3 % faster, net -5 %: profiles/r02/ab_w4_s43.jsonl.)
+constexpr int kAWin = 4;                        // bits per [a](-A) / [b](-R) window
+constexpr int kAWindows = (255 + kAWin - 1) / kAWin;  // at most: 64 x 4 = 256 bits >= 253
+constexpr int kAEntries = (1 << (kAWin - 1)) + 1;     // per-lane table 0..8 x P, cached form (entry 0 = identity)
+constexpr int kBBits = 16;                      // radix 2^16 digits of the B scalar halves
+constexpr int kBSplit = 126;                    // s = s_lo + 2^126 s_hi
+// digits per half: 8 x 16 = 128 bits for s_lo < 2^126 and s_hi < 2^127; s_hi's top
 // digit may reach 2^15, which 16-bit two's complement cannot hold: main_one reads that one digit unsigned
-constexpr int kBDigits = kAWin == 5 ? 9 : 8;
-constexpr int kBEvery = kBBits / kAWin;         // a B digit every fourth (third) window
-constexpr int kBMinWindows = kBEvery * (kBDigits - 1) + 1;  // 29 (25): the walk reaches window 28 (24)
-constexpr int kBEntries = (1 << (kBBits - 1)) + 1; // per table 0..2^15 (2^14) x base, affine precomp form, 4 (2) MiB
+constexpr int kBDigits = 8;
+constexpr int kBEvery = kBBits / kAWin;         // a B digit every fourth window
+constexpr int kBMinWindows = kBEvery * (kBDigits - 1) + 1;  // 29: the walk reaches window 28
+constexpr int kBEntries = (1 << (kBBits - 1)) + 1; // per table 0..2^15 x base, affine precomp form, 4 MiB
 constexpr int kBTables = 2;                     // base B and base 2^kBSplit B
 static_assert(kBBits % kAWin == 0, "B digits must land on window boundaries");
 constexpr int kCombEntries = 129;               // signer comb rows: 0..128 x 256^i B
@@ -241,11 +229,8 @@ EDV_HD int w8_bitlen(const uint32_t a[8]) {
   }
   return n;
 }
-#ifndef EDV_NWIN_CLZ
-#define EDV_NWIN_CLZ 1
-#endif
 EDV_HD int digits5_windows(const uint32_t d[8]) {
-  if (EDV_NWIN_CLZ && kAWin == 4) {
+  if (kAWin == 4) {
     // 4-bit fields never straddle a word: windows = ceil(bit length / 4) (the
     // per-field scan below compiled to 64 v_cndmask_b32 per scalar)
     return (w8_bitlen(d) + 3) >> 2;
@@ -679,15 +664,11 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
   // hash and lattice first, points after: the two decompressions and tables
   // then run one after the other with little else live (register pressure)
   uint32_t dig[16], h[8];
-  EDV_STAMP(1);
   hram(dig, R, A, m, mlen);
-  EDV_STAMP(2);
   sc_reduce(h, dig);
-  EDV_STAMP(3);
   uint32_t a[8], u[8];
   bool neg;
   half_scalars(h, a, u, neg);
-  EDV_STAMP(4);
   // B scalar: b S mod L with b = (neg ? -u : u)
   uint32_t s[8];
   sc_mul(s, u, S);
@@ -701,7 +682,6 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
 #pragma unroll
     for (int i = 0; i < 8; i++) s[i] = t[i];
   }
-  EDV_STAMP(5);
   recode_bscalar(pd.bw, s);
   recode5(pd.da, a);
   recode5(pd.db, u);
@@ -720,11 +700,8 @@ template <class ATab>
 EDV_HD bool prep_point(const uint32_t P[8], ATab& tab) {
   if (!ge_is_canonical(P) || has_small_order(P)) return false;
   ge_p3 nP;
-  EDV_STAMP(1);
   if (!ge_frombytes_negate(nP, P)) return false;
-  EDV_STAMP(2);
   build_table(tab, nP);
-  EDV_STAMP(3);
   return true;
 }
 
@@ -771,12 +748,6 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
       bt.stage(0, d0 < 0 ? -d0 : d0);
       bt.stage(1, d1 < 0 ? -d1 : d1);
     }
-    // diagnostic stamps (EDV_STAMPS builds only): the phases of one plain
-    // window (slots 5-10) and of the B window w = 8 (slots 11-13); the LDS
-    // picks (fetch) are memory operations, so their waits stay in place, while
-    // pure arithmetic may drift across a stamp
-    const bool sw = w == nwin - 6, sb = w == 8;
-    if (sw) EDV_STAMP(5);
     ge_p3 p3;
     if (w == nwin - 1) {
       p3 = ge_p3_identity();
@@ -785,30 +756,18 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
       for (int d = 0; d < kAWin - 1; d++) acc = ge_p1p1_to_p2(ge_p2_dbl(acc));
       p3 = ge_p1p1_to_p3(ge_p2_dbl(acc));
     }
-    if (sw) EDV_STAMP(6);
-    if (sb) EDV_STAMP(11);
     const ge_cached ea = at.fetch();
-    if (sw) EDV_STAMP(7);
     p3 = ge_p1p1_to_p3(ge_add(p3, ge_cached_cneg(ea, dA < 0)));
-    if (sw) EDV_STAMP(8);
     const ge_cached er = rt.fetch();
     if (addB) bt.issue();
-    if (sw) EDV_STAMP(9);
     ge_p1p1 t = ge_add(p3, ge_cached_cneg(er, (dR < 0) != negR));
-    if (sb) EDV_STAMP(12);
     if (addB) {
       p3 = ge_p1p1_to_p3(t);
       p3 = ge_p1p1_to_p3(ge_madd(p3, ge_precomp_cneg(bt.fetch(0), d0 < 0)));
       t = ge_madd(p3, ge_precomp_cneg(bt.fetch(1), d1 < 0));
     }
     acc = ge_p1p1_to_p2(t);
-    if (sw) EDV_STAMP(10);
-    if (sb) EDV_STAMP(13);
-    if (w == nwin - 1) EDV_STAMP(2);         // after the top window (no doublings)
-    if (w == nwin - 5) EDV_STAMP(3);         // four windows later
-    if (w == 1) EDV_STAMP(4);                // before the last window
   }
-  EDV_STAMP(14);
   // identity: X = 0 and Y = Z (mod p)
   return fe_iszero(acc.X) && fe_iszero(fe_carry32(fe_sub(acc.Y, acc.Z)));
 }

@@ -100,6 +100,10 @@ def lib():
         h.edv_profile_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
         h.edv_profile_batch_dev.restype = ctypes.c_int
+        h.edv_profile_batch_dev_flush.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int, u64,
+                                                  ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                                  ctypes.POINTER(ctypes.c_float)]
+        h.edv_profile_batch_dev_flush.restype = ctypes.c_int
         h.edv_stream.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         h.edv_stream.restype = ctypes.c_int
         h.edv_sync.argtypes = [ctypes.c_int]
@@ -108,6 +112,8 @@ def lib():
         h.edv_set_length_buckets.restype = ctypes.c_int
         h.edv_set_chunk.argtypes = [ctypes.c_int, u64]
         h.edv_set_chunk.restype = ctypes.c_int
+        h.edv_set_host_slices.argtypes = [ctypes.c_int, ctypes.c_int]
+        h.edv_set_host_slices.restype = ctypes.c_int
         h.edv_shard_split.argtypes = [vp, u64, ctypes.c_uint32, vp]
         h.edv_shard_split.restype = ctypes.c_int
         h.edv_host_alloc.argtypes = [u64, ctypes.POINTER(ctypes.c_void_p)]
@@ -181,6 +187,11 @@ def set_length_buckets(device: int, mode: int):
 def set_chunk(device: int, chunk: int):
     """Signatures per prep/main kernel pair (0 = default).  Never changes verdicts."""
     _check(lib().edv_set_chunk(device, chunk))
+
+
+def set_host_slices(device: int, slices: int):
+    """Message slices of a synchronous one-chunk shard (edv_set_host_slices; 0 = default)."""
+    _check(lib().edv_set_host_slices(device, slices))
 
 
 def _check(rc):
@@ -503,3 +514,12 @@ def profile_device(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, iters=1,
     _check(lib().edv_profile_batch_dev(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, iters,
                                        ctypes.byref(a), ctypes.byref(b)))
     return float(a.value), float(b.value)
+
+
+def profile_device_flush(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, iters=1, flush_bytes=0, msg_base=0):
+    """(prep_ms, flush_ms, main_ms) with a cache-evicting kernel of flush_bytes between
+    prep and main (edv_profile_batch_dev_flush; measurement only)."""
+    a, f, b = ctypes.c_float(0), ctypes.c_float(0), ctypes.c_float(0)
+    _check(lib().edv_profile_batch_dev_flush(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, iters,
+                                             flush_bytes, ctypes.byref(a), ctypes.byref(f), ctypes.byref(b)))
+    return float(a.value), float(f.value), float(b.value)

@@ -95,6 +95,7 @@ class PendingProd:
 
     def __init__(self, authenticator: ReqAuthenticator, client_msgs, propagates, digests: bool = True):
         self.client_msgs, self.propagates = list(client_msgs), list(propagates)
+        self.t_read = 0.0  # when the messages were read (the caller's clock), for latency bookkeeping
         self.reqs = [m["request"] for m, _frm in self.propagates] + [m for m, _frm in self.client_msgs]
         self._pending = authenticator.authenticate_batch_submit(self.reqs, digests=digests) if self.reqs else None
 

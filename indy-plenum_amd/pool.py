@@ -20,6 +20,14 @@ request signatures are verified, and reduces the rest to message counting:
 Not modelled (out of scope): view change, checkpoints,
 catch-up, BLS multi-signatures, ledgers/state execution, client replies.
 
+Request latency (what the reference's Monitor acts on, plenum/server/monitor.py:
+300-330 requestOrdered, :418-460 LAMBDA / OMEGA checks) is recorded per request
+and node: from forwarding (f+1 PROPAGATE votes, propagator.py:236-249, where
+the Monitor starts its clock) to ordering ("monitor"), from the prod that read
+the request off the node's inbox to ordering ("receipt"), and from the client's
+submission to ordering ("submit").  run_paced() offers the requests at a fixed
+rate instead of all at once, so latency is measured below saturation.
+
 Each node authenticates through a ReqAuthenticator; `batched=True` routes a
 prod's client REQUESTs and PROPAGATEs through ONE authenticate_batch call
 (node_integration.authenticate_prod), `batched=False` is the reference's
@@ -160,6 +168,11 @@ class PoolNode:
         self.busy_s = 0.0
         self.auth_s = 0.0             # time inside request authentication and request digests
         self.gc_clock = _GcClock()    # replaced by the pool's shared clock
+        # latency bookkeeping (perf_counter seconds)
+        self._pool = None
+        self._t_read = 0.0            # start of the prod that read the messages being handled
+        self.t_recv, self.t_fwd, self.key_rid = {}, {}, {}
+        self.lat = {"monitor": [], "receipt": [], "submit": []}
 
     # ------------------------------------------------------------------ I/O
     def send_all(self, msg):
@@ -175,6 +188,7 @@ class PoolNode:
     # ------------------------------------------------------------------ prod
     def prod(self, pool):
         t0 = time.perf_counter()
+        self._pool = pool
         props, three_pc = [], []
         for _ in range(min(self.node_quota, len(self.node_inbox))):
             frm, blob = self.node_inbox.popleft()
@@ -189,6 +203,7 @@ class PoolNode:
                 self.auth_calls += 1
                 with _AuthWindow(self):
                     self._pending = PendingProd(self.auth, clients, props, digests=True)
+                self._pending.t_read = t0
             if pend is not None:
                 self._finish(pend)
         elif props or clients:
@@ -197,6 +212,7 @@ class PoolNode:
             self._keys = iter(keys)
             self.verifies += len(props) + len(clients)
             self.auth_calls += 1 if self.batched else len(props) + len(clients)
+            self._t_read = t0
             authenticate_prod(self.auth, clients, props, self._on_client, self._on_propagate, self.batched)
         n_work = len(props) + len(clients) + len(three_pc) + (self._pending is not None)
         for m, frm in three_pc:
@@ -212,6 +228,7 @@ class PoolNode:
         with _AuthWindow(self):
             keys = pend.digests(self.digest_fn)
         self._keys = iter(keys)
+        self._t_read = pend.t_read
         pend.finish(self._on_client, self._on_propagate)
 
     # ------------------------------------------------------- requests
@@ -222,6 +239,7 @@ class PoolNode:
             return
         if key in self.ordered_keys:
             return                    # already ordered: the reference replies from the ledger
+        self._seen(key, req)
         self._record_and_propagate(key, req, frm)
 
     def _on_propagate(self, msg, frm, outcome):
@@ -235,7 +253,13 @@ class PoolNode:
         if st is None:
             st = self.requests[key] = _ReqState()
         st.votes.add(frm)
+        self._seen(key, msg["request"])
         self._record_and_propagate(key, msg["request"], msg.get("senderClient"))
+
+    def _seen(self, key, req):
+        if key not in self.t_recv:
+            self.t_recv[key] = self._t_read
+            self.key_rid[key] = req.get("reqId")
 
     def _record_and_propagate(self, key, req, client):
         st = self.requests.get(key)
@@ -247,6 +271,7 @@ class PoolNode:
             self.send_all({"op": "PROPAGATE", "request": req, "senderClient": client})
         if not st.forwarded and len(st.votes) >= self.f + 1:   # Quorums.propagate = f + 1
             st.forwarded = True
+            self.t_fwd[key] = time.perf_counter()   # Monitor.requestUnOrdered (propagator.py:248)
             self.finalised_set.add(key)
             if self.is_primary:
                 self.finalised.append(key)
@@ -307,7 +332,16 @@ class PoolNode:
             if s not in self.sent_commit or len(self.commits.get(s, ())) < self.n - self.f:
                 return
             keys = self.pp.pop(s)
+            now = time.perf_counter()
+            sub = self._pool.submit_t if self._pool is not None else {}
             for k in keys:
+                if k in self.t_fwd:
+                    self.lat["monitor"].append(now - self.t_fwd.pop(k))
+                if k in self.t_recv:
+                    self.lat["receipt"].append(now - self.t_recv.pop(k))
+                rid = self.key_rid.pop(k, None)
+                if rid in sub:
+                    self.lat["submit"].append(now - sub[rid])
                 self.ordered_keys.add(k)
                 self.requests.pop(k, None)
                 self.finalised_set.discard(k)
@@ -330,13 +364,48 @@ class Pool:
         self.gc_clock = _GcClock()
         for nd in self.nodes.values():
             nd.gc_clock = self.gc_clock
+        self.submit_t = {}            # reqId -> submission time
 
     def submit(self, reqs):
         """A client flood: every request sent to every node (as the client does)."""
+        now = time.perf_counter()
         for r in reqs:
             blob = json.dumps(r)
+            self.submit_t[r.get("reqId")] = now
             for node in self.nodes.values():
                 node.client_inbox.append(blob)
+
+    def run_paced(self, reqs, rate, expect=None, max_idle_s=30.0):
+        """Offer `reqs` at `rate` requests/s (request i is sent at i / rate s
+        after the start) while prodding every node round-robin, until `expect`
+        (default: all of them) are ordered on every node; returns the
+        wall-clock seconds."""
+        gc.callbacks.append(self.gc_clock)
+        try:
+            t0 = time.perf_counter()
+            sent, n = 0, len(reqs)
+            target = n if expect is None else expect
+            last_progress, last_min = t0, -1
+            while True:
+                now = time.perf_counter()
+                due = min(n, int((now - t0) * rate) + 1)
+                if due > sent:
+                    self.submit(reqs[sent:due])
+                    sent = due
+                for nd in self.nodes.values():
+                    nd.prod(self)
+                m = min(nd.ordered for nd in self.nodes.values())
+                if m >= target and sent == n:
+                    break
+                if m != last_min:
+                    last_min, last_progress = m, now
+                elif now - last_progress > max_idle_s:
+                    self.drain()
+                    raise RuntimeError("paced pool stalled: ordered %d of %d" % (m, target))
+            self.drain()
+            return time.perf_counter() - t0
+        finally:
+            gc.callbacks.remove(self.gc_clock)
 
     def run(self, expect, max_idle_rounds=50):
         """prod every node round-robin until `expect` requests are ordered on
@@ -384,4 +453,20 @@ class Pool:
                 # authentication windows; the share with every collection taken
                 # out of both node time and authentication time
                 "gc_share_of_node_time": g.total_s / node, "gc_in_auth_s": g.in_auth_s,
-                "auth_share_excluding_gc": (auth - g.in_auth_s) / max(node - g.total_s, 1e-12)}
+                "auth_share_excluding_gc": (auth - g.in_auth_s) / max(node - g.total_s, 1e-12),
+                "latency_ms": latency_summary(nodes)}
+
+
+def latency_summary(nodes):
+    """p50 / p99 / max request latency in ms over every (request, node) pair."""
+    out = {}
+    for kind, what in (("monitor", "forwarded (f+1 PROPAGATEs, the Monitor's start) -> ordered"),
+                       ("receipt", "prod that read the request off the node's inbox -> ordered"),
+                       ("submit", "client submission -> ordered")):
+        v = sorted(x for nd in nodes for x in nd.lat[kind])
+        if not v:
+            continue
+        q = lambda f: 1e3 * v[min(len(v) - 1, int(f * len(v)))]  # noqa: E731
+        out[kind] = {"p50": q(0.50), "p99": q(0.99), "max": 1e3 * v[-1], "mean": 1e3 * sum(v) / len(v),
+                     "samples": len(v), "what": what}
+    return out

@@ -14,7 +14,7 @@ _lib = None
 def load():
     global _lib
     if _lib is None:
-        srcs = [os.path.join(CSRC, f) for f in ("edv_hostcheck.cpp", "edv_math.h", "edv_verify_core.h", "edv_sha256.h")]
+        srcs = [os.path.join(CSRC, f) for f in ("edv_hostcheck.cpp", "edv_math.h", "edv_verify_core.h", "edv_sha256.h", "edv_ledger.h")]
         if not os.path.exists(SO) or os.path.getmtime(SO) < max(os.path.getmtime(s) for s in srcs):
             subprocess.check_call(["make", "-s", "-C", CSRC, "../libedv_hostcheck.so"])
         _lib = ctypes.CDLL(SO)
@@ -27,11 +27,23 @@ def load():
         _lib.hc_recode_bscalar.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
         _lib.hc_verify_batch.argtypes = [ctypes.c_char_p] * 3 + [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
         _lib.hc_layout.argtypes = [ctypes.c_void_p]
+        _lib.hc_ledger.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                   ctypes.c_void_p]
     return _lib
 
 
 def layout():
-    """The walk's layout constants as built (edv_verify_core.h, EDV_AWIN)."""
+    """The walk's layout constants as built (edv_verify_core.h)."""
     out = (ctypes.c_int32 * 7)()
     load().hc_layout(out)
     return dict(zip(("awin", "aentries", "bbits", "bsplit", "bdigits", "bevery", "bminwindows"), list(out)))
+
+
+def ledger(n, failed, queries):
+    """edv_ledger.h AsyncLedger: issue n tickets, fail `failed`, settled() per query."""
+    import numpy as np
+    f = np.asarray(failed, np.int64)
+    q = np.asarray(queries, np.int64)
+    out = np.zeros(len(q), np.int32)
+    load().hc_ledger(n, f.ctypes.data, len(f), q.ctypes.data, len(q), out.ctypes.data)
+    return out.tolist()

@@ -146,119 +146,18 @@ def test_loader_refuses_measurement_builds(tmp_path):
     bp = open(os.path.join(ROOT, "tools", "bench_pool.py")).read()
     assert 'EDV_ALLOW_MEASUREMENT_LIB="1"' in bp
 
-"""The product C-ABI library builds, loads without a GPU and exports every
-symbol include/edv.h declares; without a GPU the shim fails loudly (no CPU
-fallback)."""
-import ctypes
-import os
-import re
-import subprocess
-
-import numpy as np
-import pytest
-
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HDR = os.path.join(ROOT, "include", "edv.h")
 
 
-def declared():
-    src = open(HDR).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char \*|void)\s*\**\s*(edv_\w+)\s*\(", src, re.M)))
-
-
-def test_header_declares_the_core_entry_points():
-    names = declared()
-    for need in ("edv_verify_batch", "edv_verify_batch_dev", "edv_version", "edv_last_error", "edv_device_count",
-                 "edv_sign_batch_dev", "edv_profile_batch_dev", "edv_time_batch_dev", "edv_set_chunk"):
-        assert need in names
-
-
-def test_library_exports_every_declared_symbol():
-    from indy_plenum_amd import edv
-    lib = edv.lib()
-    missing = [n for n in declared() if not hasattr(lib, n)]
-    assert missing == []
-    out = subprocess.check_output(["nm", "-D", "--defined-only", edv.LIB_PATH]).decode()
-    exported = set(re.findall(r" T (edv_\w+)$", out, re.M))
-    assert set(declared()) <= exported
-    assert edv.version().startswith("edv ") and "gfx950" in edv.version()
-
-
-def test_library_contains_gfx950_code_object():
-    from indy_plenum_amd import edv
-    blob = open(edv.LIB_PATH, "rb").read()
-    assert b"gfx950" in blob
-    assert b"edv_main_kernel" in blob and b"edv_prep_kernel" in blob
-
-
-@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="a GPU is present")
-def test_no_gpu_means_loud_failure():
-    from indy_plenum_amd import edv
-    assert edv.device_count() == 0
-    with pytest.raises(edv.EdvUnavailable):
-        edv.verify_arrays(b"\0" * 64, b"\0" * 32, b"\0" * 16, np.array([0, 0], np.uint64))
-    with pytest.raises(edv.EdvUnavailable):
-        edv.open_batch([(b"\0" * 64, b"", b"\0" * 32)])
-
-
-def test_invalid_arguments_are_rejected_before_the_device():
-    from indy_plenum_amd import edv
-    with pytest.raises(ValueError):
-        edv.verify_arrays(b"\0" * 63, b"\0" * 32, b"", np.array([0, 0], np.uint64))
-    with pytest.raises(ValueError):
-        edv.open_batch([(b"\0" * 64, b"", b"\0" * 31)])
-    assert edv.open_batch([(b"\0" * 10, b"\0" * 10, b"\0" * 32)]) == [False]  # sm < 64: no device call
-
-
-def test_async_entry_points_validate_and_fail_loudly():
-    """edv_verify_batch_async / edv_wait_async: size mismatches are rejected in
-    the shim, a null ticket pointer and bad offsets in the C-ABI itself (before
-    any device is touched), and without a GPU a well-formed submission raises
-    EdvUnavailable rather than falling back to the CPU."""
-    import ctypes
-    from indy_plenum_amd import edv
-    sigs, pks = np.zeros(128, np.uint8), np.zeros(64, np.uint8)
-    msgs, off, acc = np.zeros(64, np.uint8), np.array([0, 16, 32], np.uint64), np.zeros(2, np.uint8)
-    with pytest.raises(ValueError):
-        edv.verify_async(sigs[:127], pks, msgs, off, acc)
-    with pytest.raises(ValueError):
-        edv.verify_async(sigs, pks, msgs, off.astype(np.int64), acc)
-    with pytest.raises(ValueError):
-        edv.verify_async(sigs, pks, msgs[:16], off, acc)
-    lib = edv.lib()
-    assert lib.edv_verify_batch_async(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, off.ctypes.data, 2,
-                                      acc.ctypes.data, 0, None) == edv.EDV_E_ARG
-    bad = np.array([0, 16, 8], np.uint64)  # offsets must not decrease
-    t = ctypes.c_int64(-1)
-    assert lib.edv_verify_batch_async(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, bad.ctypes.data, 2,
-                                      acc.ctypes.data, 0, ctypes.byref(t)) == edv.EDV_E_ARG
-    if not (os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK)):
-        with pytest.raises(edv.EdvUnavailable):
-            edv.verify_async(sigs, pks, msgs, off, acc)
-        with pytest.raises(edv.EdvUnavailable):
-            edv.wait_async(0)
-
-
-def test_product_library_is_never_the_measurement_build():
-    """The measurement-only build (variants/libedv_noverify.so: every request
-    reported valid, for bench.py's C5 comparison) is loaded only through an
-    explicit EDV_LIB in a child process; the product default is libedv.so,
-    which verifies."""
-    env_lib = os.environ.pop("EDV_LIB", None)
-    try:
-        code = ("import sys; sys.path.insert(0, %r); from indy_plenum_amd import edv; "
-                "print(edv.LIB_PATH); print(edv.version())" % ROOT)
-        r = subprocess.run(["python3", "-c", code], capture_output=True, text=True, timeout=60,
-                           env={k: v for k, v in os.environ.items() if k != "EDV_LIB"})
-        assert r.returncode == 0, r.stderr
-        path, ver = r.stdout.strip().splitlines()[-2:]
-        assert os.path.basename(path) == "libedv.so"
-        assert "MEASUREMENT-ONLY" not in ver
-    finally:
-        if env_lib is not None:
-            os.environ["EDV_LIB"] = env_lib
-    mlib = os.path.join(ROOT, "indy-plenum_amd", "variants", "libedv_noverify.so")
-    if os.path.exists(mlib):
-        m = ctypes.CDLL(mlib)
-        m.edv_version.restype = ctypes.c_char_p
-        assert b"MEASUREMENT-ONLY" in m.edv_version()
+def test_async_ledger_failures_are_sticky():
+    """the asynchronous path's ticket ledger (edv_ledger.h,
+    the code libedv.so runs, built for the CPU) never reports a failed ticket as
+    complete, however many tickets fail after it (the earlier 256-entry list
+    dropped the oldest), and reports tickets never issued as unknown."""
+    import hostcheck_lib as hc
+    E_ARG, E_HIP = -1, -3
+    failed = list(range(0, 600))                     # far more than 256 failures
+    got = hc.ledger(1000, failed, [0, 1, 255, 256, 599, 600, 999, 1000, -1])
+    assert got == [E_HIP, E_HIP, E_HIP, E_HIP, E_HIP, 0, 0, E_ARG, E_ARG]
+    # one late failure fails every earlier settled ticket (fail closed), not the later ones
+    assert hc.ledger(50, [30], [0, 29, 30, 31, 49]) == [E_HIP, E_HIP, E_HIP, 0, 0]
+    assert hc.ledger(10, [], [0, 9, 10]) == [0, 0, E_ARG]

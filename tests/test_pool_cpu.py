@@ -142,3 +142,29 @@ def test_pool_overlap_on_the_native_async_path(monkeypatch):
     assert all(k == keys[0] for k in keys) and keys[0] == set(cpu_digests(valid))
     assert calls and all(d for _n, d in calls)          # every batch asked for device digests
     assert all(issued)                                  # every queued batch was waited for
+
+
+@pytest.mark.parametrize("batched,overlap", [(False, False), (True, True)])
+def test_pool_paced_run_records_request_latency(batched, overlap, monkeypatch):
+    """run_paced offers the requests at a fixed rate and still orders every valid
+    one exactly once; every ordered (request, node) pair gets one Monitor
+    latency (forwarded -> ordered), one receipt latency and one submission
+    latency, each ordered receipt >= forwarded (a node forwards only requests it
+    has read) and submission >= receipt."""
+    monkeypatch.setattr(edv, "open_batch", lambda items, device_mask=0: H.oracle_open_batch(list(items)))
+    signers, reqs, valid = flood(n_valid=40, n_bad_sig=6, n_unknown=2, seed=11)
+    pool = Pool(factory(signers), n=4, batched=batched, digest_fn=cpu_digests, overlap=overlap, client_quota=16,
+                max_batch=7)
+    try:
+        # every request is offered; the run stops once every valid one is ordered
+        wall = pool.run_paced(reqs, rate=2000.0, expect=len(valid))
+    finally:
+        pool.close()
+    st = pool.stats(wall, len(valid))
+    assert st["ordered_per_node"] == [len(valid)] * 4
+    lat = st["latency_ms"]
+    for kind in ("monitor", "receipt", "submit"):
+        assert lat[kind]["samples"] == 4 * len(valid), kind
+        assert 0 <= lat[kind]["p50"] <= lat[kind]["p99"] <= lat[kind]["max"]
+    assert lat["receipt"]["mean"] >= lat["monitor"]["mean"]
+    assert lat["submit"]["mean"] >= lat["receipt"]["mean"]

@@ -76,7 +76,7 @@ def factory(clients, cls):
     return make
 
 
-def run(mode, clients, reqs):
+def make_pool(mode, clients, reqs):
     if mode in ("gpu_batched", "gpu_batched_overlap"):
         pool = Pool(factory(clients, CoreAuthNr), n=4, batched=True, digest_fn=digest.request_digests,
                     overlap=mode == "gpu_batched_overlap")
@@ -88,18 +88,49 @@ def run(mode, clients, reqs):
                     digest_fn=lambda rs: [table[r["reqId"]] for r in rs])
     else:
         pool = Pool(factory(clients, sodium_ref.SodiumCoreAuthNr), n=4, batched=False, digest_fn=cpu_digests)
+    return pool
+
+
+def run(mode, clients, reqs, rate=None):
+    """One pool run: the whole flood at once, or offered at `rate` requests/s."""
+    pool = make_pool(mode, clients, reqs)
     native = base58._native
     if mode == "cpu_reference":  # the reference's pure-Python base58 / serializer
         base58._native = signing_serializer._native = None
     try:
-        pool.submit(reqs)
-        wall = pool.run(len(reqs))
+        if rate:
+            wall = pool.run_paced(reqs, rate)
+        else:
+            pool.submit(reqs)
+            wall = pool.run(len(reqs))
     finally:
         pool.close()
         base58._native = signing_serializer._native = native
     st = pool.stats(wall, len(reqs))
     st["requests"] = len(reqs)
+    if rate:
+        st["offered_req_per_s"] = rate
     return st
+
+
+PACED_RATE, PACED_N = 400, 1200
+
+
+def latency_paced(clients, reqs, rate=PACED_RATE, n=PACED_N):
+    """Request latency below saturation: the same n requests offered at `rate`
+    requests/s (about 45 % of the reference flow's one-process capacity) to the
+    GPU overlap mode, the GPU batched mode and the reference flow on libsodium;
+    p50 / p99 of the Monitor's forwarded -> ordered latency and of submission ->
+    ordered, over every (request, node) pair."""
+    out = {"offered_req_per_s": rate, "requests": n,
+           "what": "run_paced: request i sent to every node at i / rate s; latencies per (request, node)"}
+    for mode in ("gpu_batched_overlap", "gpu_batched", "cpu_reference"):
+        if mode == "cpu_reference" and sodium_ref.sodium() is None:
+            continue
+        st = run(mode, clients, reqs[:n], rate=rate)
+        out[mode] = {"latency_ms": st["latency_ms"], "ordered_req_per_s_one_process": st["ordered_req_per_s_one_process"],
+                     "auth_calls": st["auth_calls"], "nacks_per_node": st["nacks_per_node"]}
+    return out
 
 
 NOVERIFY_LIB = os.path.join(ROOT, "indy-plenum_amd", "variants", "libedv_noverify.so")
@@ -136,6 +167,7 @@ def c5(n=20000, n_cpu=2000):
         out["gpu_overlap_verify_skipped"] = run_isolated("gpu_batched_overlap", n, NOVERIFY_LIB)
         out["overlap_vs_verify_skipped"] = (out["gpu_batched_overlap"]["ordered_req_per_s_one_process"]
                                             / out["gpu_overlap_verify_skipped"]["ordered_req_per_s_one_process"])
+    out["latency_paced"] = latency_paced(clients, reqs)
     ceil = out["no_verify_ceiling"]["ordered_req_per_s_one_process"]
     out["overlap_vs_ceiling"] = out["gpu_batched_overlap"]["ordered_req_per_s_one_process"] / ceil
     out["batched_vs_ceiling"] = out["gpu_batched"]["ordered_req_per_s_one_process"] / ceil
