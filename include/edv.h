@@ -197,10 +197,10 @@ int edv_profile_batch_dev_flush(const uint8_t *d_sigs, const uint8_t *d_pks, con
 int edv_set_chunk(int device, uint64_t chunk);
 
 /* Message slices of a synchronous edv_verify_batch shard that fits one chunk
- * (1..8; 0 = default 4): the messages are copied in that many slices by
- * request, and each slice's SHA-512 / scalar side runs as soon as it has
- * landed, so only the last slice's remains after the copy.  Tuning knob:
- * verdicts never depend on it. */
+ * (1..8; 0 = default: one per 65,536 requests, so one at C2): the messages are
+ * copied in that many slices by request, and each slice's SHA-512 / scalar
+ * side runs as soon as it has landed, so only the last slice's remains after
+ * the copy.  Tuning knob: verdicts never depend on it. */
 int edv_set_host_slices(int device, int slices);
 
 /* SHA-512 length buckets of the device paths (a counting sort of each chunk by

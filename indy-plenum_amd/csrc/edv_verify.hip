@@ -50,7 +50,12 @@ namespace {
 // waves/SIMD once a chunk has more than one wave per SIMD: main 5.5 % faster at
 // 2^18 signatures than with the B entries staged through LDS as well, the same
 // at 2^16, profiles/r03/ab_main_s8.jsonl).
-constexpr int kLdsAWords = 10 * 256;  // one cached entry: 10 pieces of 64 lanes x 4 words
+#ifdef EDV_PACKED_TABLES
+constexpr int kEntryPieces = 8;   // one packed entry: 8 pieces of 64 lanes x 4 words (LDS)
+#else
+constexpr int kEntryPieces = 10;  // one cached entry: 10 pieces of 64 lanes x 4 words
+#endif
+constexpr int kLdsAWords = kEntryPieces * 256;
 constexpr int kLdsWaveWords = 2 * kLdsAWords;
 __device__ __forceinline__ void wait_staged() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 struct LdsATab {
@@ -58,24 +63,32 @@ struct LdsATab {
   int32_t* lds;         // the wave's LDS region for this table
   int lane;
   __device__ __forceinline__ void stage(int e) {
-    const int32_t* g = slot + e * 40;
+    const int32_t* g = slot + e * kEntryWords;
 #pragma unroll
-    for (int q = 0; q < 10; q++)
+    for (int q = 0; q < kEntryPieces; q++)
       __builtin_amdgcn_global_load_lds(const_cast<int32_t*>(g + 4 * q), lds + q * 256, 16, 0, 0);
   }
   __device__ __forceinline__ ge_cached fetch() {
     wait_staged();
-    int32_t t[40];
+    int32_t t[4 * kEntryPieces];
 #pragma unroll
-    for (int q = 0; q < 10; q++) {
+    for (int q = 0; q < kEntryPieces; q++) {
       const int4 v = reinterpret_cast<const int4*>(lds + q * 256)[lane];
       t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
     }
     ge_cached c;
+#ifdef EDV_PACKED_TABLES
+    const uint32_t* u = reinterpret_cast<const uint32_t*>(t);
+    c.YpX = fe_unpack(u);
+    c.YmX = fe_unpack(u + 8);
+    c.Z = fe_unpack(u + 16);
+    c.T2d = fe_unpack(u + 24);
+#else
 #pragma unroll
     for (int l = 0; l < 10; l++) {
       c.YpX.v[l] = t[l]; c.YmX.v[l] = t[10 + l]; c.Z.v[l] = t[20 + l]; c.T2d.v[l] = t[30 + l];
     }
+#endif
     return c;
   }
 };
@@ -380,7 +393,7 @@ constexpr int kQ = 4;
 // Message slices of the synchronous field-ordered path (run_shard_fields): the
 // hash side of slice k runs while slice k+1 copies.  edv_set_host_slices.
 constexpr int kSlices = 8;
-constexpr int kSlicesDefault = 4;
+constexpr uint64_t kMinSliceReqs = 65536;
 // In-flight batches of the asynchronous host path per device: a Node keeps one
 // per prod in flight, and a pool of nodes in one process (C5) one per node, so
 // eight slots let up to eight callers overlap before a submission has to wait.
@@ -432,7 +445,7 @@ struct DevCtx {
   hipStream_t hcp = nullptr;
   hipEvent_t part_copied[kQ] = {}, part_prepped[kQ] = {};
   hipEvent_t slice_copied[kSlices] = {}, slice_hashed[kSlices] = {};
-  int host_slices = kSlicesDefault;
+  int host_slices = 0;              // 0 = one slice per kMinSliceReqs requests
   // asynchronous host path (edv_verify_batch_async): kAsyncSlots slots used in turn,
   // H2D copies on hcp, kernels and the verdicts' D2H on hac, so the copies of
   // batch k+1 run while batch k computes
@@ -926,8 +939,13 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
   const uint64_t n = hi - lo, mbase = off[lo], mbytes = off[hi] - mbase;
   const hipStream_t cp = c.hcp, s0 = c.hs[0];
   const bool bucket = bucketing_enabled(c, varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH);
-  // slices of whole workgroups (256 requests), at most kSlices
-  int K = bucket ? 1 : c.host_slices;
+  // one slice per 65,536 requests (a slice's hash side takes a whole wave's
+  // latency at any size below that, so smaller slices only add copy gaps:
+  // profiles/r05/trace_sync_s1.json), at most kSlices; edv_set_host_slices
+  // overrides; a bucketed shard is one slice
+  int K = bucket ? 1 : (c.host_slices ? c.host_slices : int(n / kMinSliceReqs));
+  if (K < 1) K = 1;
+  if (K > kSlices) K = kSlices;
   if (uint64_t(K) * kBlock > n) K = int(n / kBlock) > 1 ? int(n / kBlock) : 1;
   uint64_t rb[kSlices + 1], mb[kSlices + 1];  // request / message-byte bounds of the slices (shard-relative)
   for (int k = 0; k <= K; k++) {
@@ -935,9 +953,13 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
     mb[k] = off[lo + rb[k]] - mbase;
   }
   // the scratch's previous users (any stream) finish before the kernels write it,
-  // and the copies follow the previous call's
-  HIPOK(hipStreamWaitEvent(cp, c.st_done, 0), "wait scratch");
-  for (int q = 0; q < kQ; q++) HIPOK(hipStreamWaitEvent(c.hs[q], c.st_done, 0), "wait scratch");
+  // and the copies follow the previous call's (nothing to wait for when its
+  // last user is already done, e.g. the previous synchronous call)
+  if (hipEventQuery(c.st_done) != hipSuccess) {
+    (void)hipGetLastError();
+    HIPOK(hipStreamWaitEvent(cp, c.st_done, 0), "wait scratch");
+    for (int q = 0; q < kQ; q++) HIPOK(hipStreamWaitEvent(c.hs[q], c.st_done, 0), "wait scratch");
+  }
   const uint8_t *src_s = sigs + 64 * lo, *src_p = pks + 32 * lo, *src_m = msgs + mbase;
   const uint8_t* src_o = reinterpret_cast<const uint8_t*>(off + lo);
   PinnedBuf& sl = c.stage[0];
@@ -1005,8 +1027,10 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
 // from the caller's memory when it is pinned, else through this stream's
 // pinned slot, filled by a parallel memcpy while earlier sub-batches run),
 // [length buckets,] prep, main, D2H of its accept bytes.  Caller holds c.mu.
+// uniform: every message of the whole batch has one SHA-512 block count (known
+// from the argument check), else the shard is scanned for it.
 int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off, uint64_t lo,
-              uint64_t hi, uint8_t* accept) {
+              uint64_t hi, uint8_t* accept, bool uniform) {
   const uint64_t n = hi - lo;
   if (n == 0) return 0;
   // A shard that fits one chunk is one sub-batch on one stream: split 2 or 4
@@ -1030,7 +1054,7 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
   const bool acc_pinned = is_pinned(accept + lo);
   if (!acc_pinned && c.acc_host.ensure(n)) return EDV_E_OOM;
   // bucket by SHA block count only when the shard's messages differ in block count
-  const bool varied = !scan_offsets(off, lo, hi).uniform;
+  const bool varied = !uniform && !scan_offsets(off, lo, hi).uniform;
   const uint32_t flags = varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH;
   uint8_t* d_sigs = static_cast<uint8_t*>(c.sigs.p);
   uint8_t* d_pks = static_cast<uint8_t*>(c.pks.p);
@@ -1152,7 +1176,7 @@ int async_complete(DevCtx& c, DevCtx::AsyncSlot& s) {
 // slot's own stream and scratch instead.  A slot is reused kAsyncSlots
 // submissions later, after its batch is complete.  Caller holds c.mu.
 int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
-                 uint64_t n, uint8_t* accept, uint8_t* digests, int64_t* ticket) {
+                 uint64_t n, uint8_t* accept, uint8_t* digests, bool uniform, int64_t* ticket) {
   const int64_t t = c.ledger.next;
   DevCtx::AsyncSlot& s = c.as[t % kAsyncSlots];
   int err;
@@ -1176,7 +1200,7 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
   const bool pinned = is_pinned(sigs) && is_pinned(pks) && is_pinned(off) && (mbytes == 0 || is_pinned(msgs + mbase));
   s.acc_pinned = is_pinned(accept);
   if (!s.acc_pinned && s.acc_host.ensure(n)) return EDV_E_OOM;
-  const bool varied = !scan_offsets(off, 0, n).uniform;
+  const bool varied = !uniform;
   const uint32_t lflags = varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH;
   const uint8_t *src_s = sigs, *src_p = pks, *src_m = msgs + mbase;
   const uint8_t* src_o = reinterpret_cast<const uint8_t*>(off);
@@ -1230,11 +1254,11 @@ constexpr uint64_t kVerifyBlocks = 40;
 // Split [0, n) into g contiguous shards by request index: equal counts when
 // every message has the same SHA-512 block count (C2/C3), else equal estimated
 // cost, sum over the shard of (kVerifyBlocks + blocks_i) (C4).
-void shard_bounds(const uint64_t* off, uint64_t n, uint32_t g, uint64_t* b) {
+void shard_bounds(const uint64_t* off, uint64_t n, uint32_t g, uint64_t* b, int uniform = -1) {
   b[0] = 0;
   b[g] = n;
   if (g == 1) return;
-  if (n == 0 || scan_offsets(off, 0, n).uniform) {
+  if (n == 0 || uniform == 1 || (uniform < 0 && scan_offsets(off, 0, n).uniform)) {
     for (uint32_t k = 1; k < g; k++) b[k] = uint64_t((unsigned __int128)n * k / g);
     return;
   }
@@ -1291,16 +1315,16 @@ int device_load(int d) {
 }
 
 // Placement of the g shards of a batch on g of the devices `devs` (g == 1: a
-// batch that runs on one device).  Preference: initialised devices with nothing
-// running (so a process that verifies one batch at a time stays on its
-// contexts); then devices not yet initialised, in an order that starts at pid
-// mod ndev (the processes of a node spread over its GPUs); then the least-loaded
-// busy devices.  Load = synchronous calls placed on the device + its asynchronous
+// batch that runs on one device).  Preference: initialised devices whose load is
+// below `busy_at` (1 for synchronous calls: nothing running; so a process that
+// verifies one batch at a time stays on its contexts); then devices not yet
+// initialised, in an order that starts at pid mod ndev (the processes of a node
+// spread over its GPUs); then the least-loaded busy devices.  Load = synchronous calls placed on the device + its asynchronous
 // batches still running.  Chosen devices are reserved (running + 1) under one
 // placement lock, so concurrent callers see each other's choices; the caller
 // releases them (Placed).
 std::mutex g_place_mu;
-std::vector<int> place(const std::vector<int>& devs, uint32_t g) {
+std::vector<int> place(const std::vector<int>& devs, uint32_t g, int busy_at = 1) {
   const int k = int(devs.size());
   std::vector<int> out;
   std::lock_guard<std::mutex> lk(g_place_mu);
@@ -1318,7 +1342,7 @@ std::vector<int> place(const std::vector<int>& devs, uint32_t g) {
         continue;
       }
       const int load = device_load(d);
-      if (load == 0) idle.push_back(d);
+      if (load < busy_at) idle.push_back(d);
       else busy.push_back({load, d});
     }
     std::stable_sort(busy.begin(), busy.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
@@ -1330,9 +1354,15 @@ std::vector<int> place(const std::vector<int>& devs, uint32_t g) {
   for (int d : out) g_ctx[d]->running.fetch_add(1);
   return out;
 }
+// The asynchronous path's pick (edv_pick_device): an initialised device with
+// fewer than two batches running still counts as free -- a Node that keeps one
+// prod's batch in flight while it submits the next stays on its context (small
+// batches run side by side on their slots' own streams, kSmallAsync), while
+// several nodes' prods in flight together spread over the GPUs.
+constexpr int kAsyncBusyAt = 2;
 int pick_device(const std::vector<int>& devs) {
   if (devs.size() == 1) return devs[0];
-  const int d = place(devs, 1)[0];
+  const int d = place(devs, 1, kAsyncBusyAt)[0];
   g_ctx[d]->running.fetch_sub(1);  // a pick only advises (edv_pick_device): no reservation kept
   return d;
 }
@@ -1360,7 +1390,7 @@ std::vector<int> devices_of(uint32_t device_mask, int* err) {
 // that is one shard runs on the calling thread.  The devices are place()'s
 // choice.  shard(ctx, lo, hi) does the work under the context lock.
 template <class Shard>
-int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard shard) {
+int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard shard, int uniform = -1) {
   int err;
   std::vector<int> devs = devices_of(device_mask, &err);
   if (err) return err;
@@ -1377,7 +1407,7 @@ int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard 
   };
   if (g == 1) return one(on[0], 0, n);
   std::vector<uint64_t> bounds(g + 1);
-  shard_bounds(off, n, g, bounds.data());
+  shard_bounds(off, n, g, bounds.data(), uniform);
   std::vector<int> rc(g, 0);
   std::vector<std::string> errs(g);
   std::vector<std::thread> th;
@@ -1393,8 +1423,12 @@ int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard 
   return 0;
 }
 
-int check_offsets(const uint64_t* msg_off, uint64_t n) {
-  if (!scan_offsets(msg_off, 0, n).ok) return set_err(EDV_E_ARG, "msg_off not non-decreasing");
+// One pass over the offsets: valid (non-decreasing), and -- into *uniform if
+// asked -- whether every message has the same SHA-512 block count.
+int check_offsets(const uint64_t* msg_off, uint64_t n, bool* uniform = nullptr) {
+  const OffScan sc = scan_offsets(msg_off, 0, n);
+  if (!sc.ok) return set_err(EDV_E_ARG, "msg_off not non-decreasing");
+  if (uniform) *uniform = sc.uniform;
   return 0;
 }
 
@@ -1457,11 +1491,13 @@ int edv_verify_batch(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msg
   if (!sigs || !pks || !msg_off || !accept) return set_err(EDV_E_ARG, "null pointer");
   if (!msgs && msg_off[n] != msg_off[0]) return set_err(EDV_E_ARG, "null msgs");
   int err;
-  if ((err = check_offsets(msg_off, n))) return err;
+  bool uniform = false;
+  if ((err = check_offsets(msg_off, n, &uniform))) return err;
   memset(accept, 0, n);  // fail closed: a call that fails part-way leaves rejections
-  return for_each_shard(msg_off, n, device_mask, [&](DevCtx& c, uint64_t lo, uint64_t hi) {
-    return run_shard(c, sigs, pks, msgs, msg_off, lo, hi, accept);
-  });
+  return for_each_shard(
+      msg_off, n, device_mask,
+      [&](DevCtx& c, uint64_t lo, uint64_t hi) { return run_shard(c, sigs, pks, msgs, msg_off, lo, hi, accept, uniform); },
+      uniform ? 1 : 0);
 }
 
 int edv_verify_batch_async(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* msg_off,
@@ -1477,14 +1513,15 @@ int edv_verify_digest_batch_async(const uint8_t* sigs, const uint8_t* pks, const
   if (n > 0 && (!sigs || !pks || !msg_off || !accept)) return set_err(EDV_E_ARG, "null pointer");
   if (n > 0 && !msgs && msg_off[n] != msg_off[0]) return set_err(EDV_E_ARG, "null msgs");
   int err;
-  if (n > 0 && (err = check_offsets(msg_off, n))) return err;
+  bool uniform = false;
+  if (n > 0 && (err = check_offsets(msg_off, n, &uniform))) return err;
   CtxLock cl(device);
   if (cl.err) return cl.err;
   if (n == 0) {
     *ticket = cl.c->ledger.issue();
     return 0;
   }
-  if ((err = submit_async(*cl.c, sigs, pks, msgs, msg_off, n, accept, digests, ticket))) {
+  if ((err = submit_async(*cl.c, sigs, pks, msgs, msg_off, n, accept, digests, uniform, ticket))) {
     // whatever was queued before the failure may still read the caller's
     // buffers: let it finish before the caller gets the error back
     (void)hipStreamSynchronize(cl.c->hcp);
@@ -1709,7 +1746,7 @@ int edv_set_host_slices(int device, int slices) {
   if (!c) return err;
   if (slices < 0 || slices > kSlices) return set_err(EDV_E_ARG, "slices must be 0..8");
   std::lock_guard<std::mutex> lk(c->mu);
-  c->host_slices = slices ? slices : kSlicesDefault;
+  c->host_slices = slices;
   return 0;
 }
 

@@ -1,10 +1,13 @@
 """Multi-GPU sharding of a verify batch by request index.
 
 Verification has no exchange step: shard k of G gets a contiguous index range
-and nothing crosses devices until the per-request accept bytes are gathered
-back into request order (host memcpy in edv_verify_batch; an all-gather over
-torch.distributed -- RCCL over xGMI -- in the one-process-per-GPU layout
-bench.py uses, which lives in bench.py, not in this package).
+and nothing crosses devices until the verdicts are gathered back into request
+order: the shards' accept bytes land in their slices of the caller's array in
+edv_verify_batch (one host thread per device); in bench.py's
+one-process-per-GPU layout each rank packs its verdicts into a bitmask on its
+GPU (edv_pack_bits_dev, N/8 bytes), copies it to the host and sends it to rank
+0 over a loopback TCP rendezvous after the timed region (no torch, no RCCL:
+nothing in the product or the bench needs a collective).
 
 Two splits:
   shard_range   equal counts, [k*N/G, (k+1)*N/G)   (C2/C3: one message length)

@@ -9,8 +9,12 @@ run_counter_collection.csv rocprofv3 wrote.
 
 HBM (MI355X_MICROARCH.md "HBM"): on gfx950 FETCH_SIZE reports half the bytes of
 wide coalesced reads, so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact
-(x 1024).  Infinity-Cache (MALL) hits are counted by these counters, not
-excluded, so the figure is an upper bound on DRAM traffic.
+(x 1024).  When the pass with the request-size counters (TCC_EA0_RDREQ_{32B,64B,
+128B}_sum) is present, read bytes come from them instead (calibrated on known
+byte counts for the main kernel's gather pattern, tools/ubench_gather.hip), and
+the FETCH_SIZE figure is kept as a cross-check.  Infinity-Cache (MALL) hits are
+counted by these counters, not excluded, so the figure is an upper bound on
+DRAM traffic.
 
 VALU: SQ_INSTS_VALU counts wave-instructions (one per wave per VALU
 instruction); SQ_ACTIVE_INST_VALU counts them in quad-cycles; GRBM_GUI_ACTIVE
@@ -64,6 +68,18 @@ def summarise(root):
             d["read_bytes"] = 2 * avg.get("FETCH_SIZE", 0.0) * 1024
             d["write_bytes"] = avg.get("WRITE_SIZE", 0.0) * 1024
             d["hbm_bytes_per_launch"] = d["read_bytes"] + d["write_bytes"]
+        if "TCC_EA0_RDREQ_128B_sum" in avg:
+            # calibrated (profiles/r05/gather_calibration.json): the L2's fabric read
+            # requests by size; bytes = 128 x (128-B) + 64 x (64-B) + 32 x (32-B)
+            # requests, exact for a known streamed byte count and for the main
+            # kernel's per-lane 160-B gather alike
+            d["read_bytes_by_request_size"] = (128 * avg["TCC_EA0_RDREQ_128B_sum"]
+                                               + 64 * avg.get("TCC_EA0_RDREQ_64B_sum", 0.0)
+                                               + 32 * avg.get("TCC_EA0_RDREQ_32B_sum", 0.0))
+            if "read_bytes" in d:
+                d["read_bytes_fetch_vs_request_size"] = d["read_bytes"] / max(d["read_bytes_by_request_size"], 1.0)
+                d["read_bytes"] = d["read_bytes_by_request_size"]
+                d["hbm_bytes_per_launch"] = d["read_bytes"] + d["write_bytes"]
         if "SQ_INSTS_VALU" in avg and avg.get("SQ_WAVES"):
             d["valu_insts_per_wave"] = avg["SQ_INSTS_VALU"] / avg["SQ_WAVES"]
             d["salu_insts_per_wave"] = avg.get("SQ_INSTS_SALU", 0.0) / avg["SQ_WAVES"]
