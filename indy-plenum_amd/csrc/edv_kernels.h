@@ -15,13 +15,7 @@
 namespace edv {
 
 constexpr int kBlock = 256;
-#ifdef EDV_PACKED_TABLES
-// cached point = 4 canonical 255-bit encodings (fe_tobytes), 32 words = 128 B:
-// one 128-byte line per gathered entry (9 entries: 288 words = 1,152 B)
-constexpr int kEntryWords = 32;
-#else
 constexpr int kEntryWords = 40;           // cached point = 4 x 10 limbs, 160 B
-#endif
 constexpr int kAWords = kAEntries * kEntryWords;  // per-signature table (9 entries: 360 words = 1,440 B)
 // dig words per signature: da (8), db (8), B digit pairs (kBDigits), window count (1)
 constexpr int kDigWords = 8 + 8 + kBDigits + 1;
@@ -69,21 +63,10 @@ struct VerifyArgs {
 // 39 KB of L2-miss traffic per verify, 8x the useful bytes).
 struct GlobalATab {
   int32_t* slot;
-#ifdef EDV_PACKED_TABLES
-  // one entry = 32 contiguous words (128 B, 128-byte aligned when the slot is):
-  // the four coordinates' canonical encodings, eight 16-byte stores
-  __device__ __forceinline__ void store(int e, const ge_cached& c) const {
-    uint32_t t[32];
-    fe_tobytes(t, fe_carry32(c.YpX));
-    fe_tobytes(t + 8, fe_carry32(c.YmX));
-    fe_tobytes(t + 16, fe_carry32(c.Z));
-    fe_tobytes(t + 24, fe_carry32(c.T2d));
-    uint4* p = reinterpret_cast<uint4*>(slot + e * kEntryWords);
-#pragma unroll
-    for (int q = 0; q < 8; q++) p[q] = make_uint4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
-  }
-#else
-  // one entry = 40 contiguous words (160 B, 16-byte aligned): ten 16-byte stores
+  // one entry = 40 contiguous words (160 B, 16-byte aligned): ten 16-byte stores.
+  // (Packing an entry into 128 B -- four canonical 255-bit encodings, one line
+  // per gather -- halved main's fabric reads but made the C2 step 3.4 % slower:
+  // profiles/r05/ab_packed_s2.jsonl.)
   __device__ __forceinline__ void store(int e, const ge_cached& c) const {
     int32_t t[40];
 #pragma unroll
@@ -94,7 +77,6 @@ struct GlobalATab {
 #pragma unroll
     for (int q = 0; q < 10; q++) p[q] = make_int4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
   }
-#endif
 };
 // Shared 0..2^15 x B and 0..2^15 x 2^126 B tables in global memory (2 x 4 MiB,
 // L2/MALL-resident), read as 16-byte vectors: too large for LDS, and each lane

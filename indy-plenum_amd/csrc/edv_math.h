@@ -355,24 +355,6 @@ EDV_HD fe fe_frombytes(const uint32_t w[8]) {
   return fe_carry32(h);
 }
 
-// fe_frombytes without the final carry, for the canonical (< p) encodings the
-// prep kernel packs table entries into: every limb is already in [0, 2^26) /
-// [0, 2^25), which products and squarings accept as they stand.
-EDV_HD fe fe_unpack(const uint32_t w[8]) {
-  fe h;
-  h.v[0] = w[0] & 0x3ffffff;
-  h.v[1] = ((w[0] >> 26) | (w[1] << 6)) & 0x1ffffff;
-  h.v[2] = ((w[1] >> 19) | (w[2] << 13)) & 0x3ffffff;
-  h.v[3] = ((w[2] >> 13) | (w[3] << 19)) & 0x1ffffff;
-  h.v[4] = (w[3] >> 6) & 0x3ffffff;
-  h.v[5] = w[4] & 0x1ffffff;
-  h.v[6] = ((w[4] >> 25) | (w[5] << 7)) & 0x3ffffff;
-  h.v[7] = ((w[5] >> 19) | (w[6] << 13)) & 0x1ffffff;
-  h.v[8] = ((w[6] >> 12) | (w[7] << 20)) & 0x3ffffff;
-  h.v[9] = (w[7] >> 6) & 0x1ffffff;
-  return h;
-}
-
 EDV_HD bool fe_iszero(const fe& f) {
   uint32_t w[8];
   fe_tobytes(w, f);

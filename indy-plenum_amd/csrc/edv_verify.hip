@@ -50,11 +50,7 @@ namespace {
 // waves/SIMD once a chunk has more than one wave per SIMD: main 5.5 % faster at
 // 2^18 signatures than with the B entries staged through LDS as well, the same
 // at 2^16, profiles/r03/ab_main_s8.jsonl).
-#ifdef EDV_PACKED_TABLES
-constexpr int kEntryPieces = 8;   // one packed entry: 8 pieces of 64 lanes x 4 words (LDS)
-#else
 constexpr int kEntryPieces = 10;  // one cached entry: 10 pieces of 64 lanes x 4 words
-#endif
 constexpr int kLdsAWords = kEntryPieces * 256;
 constexpr int kLdsWaveWords = 2 * kLdsAWords;
 __device__ __forceinline__ void wait_staged() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -77,18 +73,10 @@ struct LdsATab {
       t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
     }
     ge_cached c;
-#ifdef EDV_PACKED_TABLES
-    const uint32_t* u = reinterpret_cast<const uint32_t*>(t);
-    c.YpX = fe_unpack(u);
-    c.YmX = fe_unpack(u + 8);
-    c.Z = fe_unpack(u + 16);
-    c.T2d = fe_unpack(u + 24);
-#else
 #pragma unroll
     for (int l = 0; l < 10; l++) {
       c.YpX.v[l] = t[l]; c.YmX.v[l] = t[10 + l]; c.Z.v[l] = t[20 + l]; c.T2d.v[l] = t[30 + l];
     }
-#endif
     return c;
   }
 };
@@ -468,6 +456,7 @@ struct DevCtx {
   // so nothing is copied into the caller's buffers afterwards
   AsyncLedger ledger;
   DevBuf sigs, pks, msgs, off, acc;
+  DevBuf fblob;  // the field path's signatures | keys | offsets block when they arrive in one copy
   PinnedBuf stage[kQ], acc_host;
   // Pipelined submission (edv_verify_batch_dev_pipelined): two state sets, a
   // prep stream and a main stream, so the prep kernel of batch k+1 runs on the
@@ -933,25 +922,15 @@ OffScan scan_offsets(const uint64_t* off, uint64_t lo, uint64_t hi) {
 // verdicts' D2H.  Length-bucketed shards (messages of several SHA-512 block
 // counts) hash in one piece after the whole copy: the bucket permutation
 // spans the shard.  Caller holds c.mu.
+// uniform: 1 / 0 = the offsets were checked and every message has (not) one
+// SHA-512 block count; -1 = not checked yet: the check runs here, on the host,
+// while the first copy (whose size depends on n only) is already on its way,
+// and a failed check returns EDV_E_ARG before anything reads the offsets.
 int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
-                     uint64_t lo, uint64_t hi, bool pinned, bool varied, uint8_t* d_sigs, uint8_t* d_pks,
+                     uint64_t lo, uint64_t hi, bool pinned, int uniform, uint8_t* d_sigs, uint8_t* d_pks,
                      uint8_t* d_msgs, uint64_t* d_off, uint8_t* d_acc, uint8_t* h_acc) {
   const uint64_t n = hi - lo, mbase = off[lo], mbytes = off[hi] - mbase;
   const hipStream_t cp = c.hcp, s0 = c.hs[0];
-  const bool bucket = bucketing_enabled(c, varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH);
-  // one slice per 65,536 requests (a slice's hash side takes a whole wave's
-  // latency at any size below that, so smaller slices only add copy gaps:
-  // profiles/r05/trace_sync_s1.json), at most kSlices; edv_set_host_slices
-  // overrides; a bucketed shard is one slice
-  int K = bucket ? 1 : (c.host_slices ? c.host_slices : int(n / kMinSliceReqs));
-  if (K < 1) K = 1;
-  if (K > kSlices) K = kSlices;
-  if (uint64_t(K) * kBlock > n) K = int(n / kBlock) > 1 ? int(n / kBlock) : 1;
-  uint64_t rb[kSlices + 1], mb[kSlices + 1];  // request / message-byte bounds of the slices (shard-relative)
-  for (int k = 0; k <= K; k++) {
-    rb[k] = k == K ? n : (n * k / K) / kBlock * kBlock;
-    mb[k] = off[lo + rb[k]] - mbase;
-  }
   // the scratch's previous users (any stream) finish before the kernels write it,
   // and the copies follow the previous call's (nothing to wait for when its
   // last user is already done, e.g. the previous synchronous call)
@@ -970,9 +949,46 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
     par_copy({{p, src_s, 64 * n}, {p + 64 * n, src_p, 32 * n}, {p + 96 * n, src_o, 8 * (n + 1)}});
     src_s = p; src_p = p + 64 * n; src_o = p + 96 * n;
   }
-  HIPOK(hipMemcpyAsync(d_sigs, src_s, n * 64, hipMemcpyHostToDevice, cp), "h2d sigs");
-  HIPOK(hipMemcpyAsync(d_pks, src_p, n * 32, hipMemcpyHostToDevice, cp), "h2d pks");
-  HIPOK(hipMemcpyAsync(d_off, src_o, (n + 1) * 8, hipMemcpyHostToDevice, cp), "h2d off");
+  // Signatures, keys and offsets that lie in one host region in that order
+  // (always so once staged; so for a caller that packs a batch into one
+  // pinned buffer) go in ONE copy into a device block of the same layout: each
+  // separate copy costs the DMA engine a gap (~12 us each, trace_sync).
+  const uint64_t gp = uint64_t(src_p - src_s), go = uint64_t(src_o - src_s), span = go + 8 * (n + 1);
+  if (src_p >= src_s + 64 * n && src_o >= src_p + 32 * n && span <= 104 * n + 8 + 4096 && gp % 16 == 0 &&
+      go % 8 == 0) {
+    if (c.fblob.ensure(span)) return EDV_E_OOM;
+    uint8_t* blob = static_cast<uint8_t*>(c.fblob.p);
+    d_sigs = blob;
+    d_pks = blob + gp;
+    d_off = reinterpret_cast<uint64_t*>(blob + go);
+    HIPOK(hipMemcpyAsync(blob, src_s, span, hipMemcpyHostToDevice, cp), "h2d sigs+pks+off");
+  } else {
+    HIPOK(hipMemcpyAsync(d_sigs, src_s, n * 64, hipMemcpyHostToDevice, cp), "h2d sigs");
+    HIPOK(hipMemcpyAsync(d_pks, src_p, n * 32, hipMemcpyHostToDevice, cp), "h2d pks");
+    HIPOK(hipMemcpyAsync(d_off, src_o, (n + 1) * 8, hipMemcpyHostToDevice, cp), "h2d off");
+  }
+  if (uniform < 0) {
+    const OffScan sc = scan_offsets(off, lo, hi);
+    if (!sc.ok) {
+      HIPOK(hipStreamSynchronize(cp), "stream sync");  // nothing may read the caller's buffers after we return
+      return set_err(EDV_E_ARG, "msg_off not non-decreasing");
+    }
+    uniform = sc.uniform ? 1 : 0;
+  }
+  const bool bucket = bucketing_enabled(c, uniform ? EDV_FLAG_UNIFORM_LENGTH : EDV_FLAG_BUCKETS);
+  // one slice per 65,536 requests (a slice's hash side takes a whole wave's
+  // latency at any size below that, so smaller slices only add copy gaps:
+  // profiles/r05/trace_sync_s1.json), at most kSlices; edv_set_host_slices
+  // overrides; a bucketed shard is one slice
+  int K = bucket ? 1 : (c.host_slices ? c.host_slices : int(n / kMinSliceReqs));
+  if (K < 1) K = 1;
+  if (K > kSlices) K = kSlices;
+  if (uint64_t(K) * kBlock > n) K = int(n / kBlock) > 1 ? int(n / kBlock) : 1;
+  uint64_t rb[kSlices + 1], mb[kSlices + 1];  // request / message-byte bounds of the slices (shard-relative)
+  for (int k = 0; k <= K; k++) {
+    rb[k] = k == K ? n : (n * k / K) / kBlock * kBlock;
+    mb[k] = off[lo + rb[k]] - mbase;
+  }
   HIPOK(hipEventRecord(c.part_copied[0], cp), "record");
   int err;
   // the point sides first: they need only what has just been queued
@@ -1027,10 +1043,12 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
 // from the caller's memory when it is pinned, else through this stream's
 // pinned slot, filled by a parallel memcpy while earlier sub-batches run),
 // [length buckets,] prep, main, D2H of its accept bytes.  Caller holds c.mu.
-// uniform: every message of the whole batch has one SHA-512 block count (known
-// from the argument check), else the shard is scanned for it.
+// uniform: 1 = every message of the whole batch has one SHA-512 block count
+// (known from the argument check), 0 = not, so the shard is scanned for it;
+// -1 = the offsets are not checked yet (a large one-shard call: the field path
+// checks them while its first copy runs, the other paths first thing).
 int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off, uint64_t lo,
-              uint64_t hi, uint8_t* accept, bool uniform) {
+              uint64_t hi, uint8_t* accept, int uniform) {
   const uint64_t n = hi - lo;
   if (n == 0) return 0;
   // A shard that fits one chunk is one sub-batch on one stream: split 2 or 4
@@ -1045,6 +1063,12 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
   P = ((P + 63) / 64) * 64;
   if (P > pmax) P = pmax;
   const uint64_t nsub = (n + P - 1) / P;
+  if (uniform < 0 && nsub != 1) {
+    const OffScan sc = scan_offsets(off, lo, hi);
+    if (!sc.ok) return set_err(EDV_E_ARG, "msg_off not non-decreasing");
+    uniform = sc.uniform ? 1 : 0;
+  }
+  if (uniform == 0) uniform = scan_offsets(off, lo, hi).uniform ? 1 : 0;  // this shard may be uniform
   const uint64_t mbase = off[lo], mbytes = off[hi] - off[lo];
   if (c.sigs.ensure(n * 64) || c.pks.ensure(n * 32) || c.msgs.ensure(mbytes + 64) ||
       c.off.ensure((n + nsub) * 8) || c.acc.ensure(n))
@@ -1054,8 +1078,7 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
   const bool acc_pinned = is_pinned(accept + lo);
   if (!acc_pinned && c.acc_host.ensure(n)) return EDV_E_OOM;
   // bucket by SHA block count only when the shard's messages differ in block count
-  const bool varied = !uniform && !scan_offsets(off, lo, hi).uniform;
-  const uint32_t flags = varied ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH;
+  const uint32_t flags = uniform == 0 ? EDV_FLAG_BUCKETS : EDV_FLAG_UNIFORM_LENGTH;
   uint8_t* d_sigs = static_cast<uint8_t*>(c.sigs.p);
   uint8_t* d_pks = static_cast<uint8_t*>(c.pks.p);
   uint8_t* d_msgs = static_cast<uint8_t*>(c.msgs.p);
@@ -1066,7 +1089,7 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
   // One chunk: copied field by field, the point sides starting before the
   // messages are in.
   if (nsub == 1) {
-    if ((err = run_shard_fields(c, sigs, pks, msgs, off, lo, hi, pinned, varied, d_sigs, d_pks, d_msgs, d_off,
+    if ((err = run_shard_fields(c, sigs, pks, msgs, off, lo, hi, pinned, uniform, d_sigs, d_pks, d_msgs, d_off,
                                 d_acc, h_acc)))
       return err;
     if (!acc_pinned) memcpy(accept + lo, h_acc, n);
@@ -1425,6 +1448,7 @@ int for_each_shard(const uint64_t* off, uint64_t n, uint32_t device_mask, Shard 
 
 // One pass over the offsets: valid (non-decreasing), and -- into *uniform if
 // asked -- whether every message has the same SHA-512 block count.
+constexpr uint64_t kDeferScanMin = 16384;  // see edv_verify_batch
 int check_offsets(const uint64_t* msg_off, uint64_t n, bool* uniform = nullptr) {
   const OffScan sc = scan_offsets(msg_off, 0, n);
   if (!sc.ok) return set_err(EDV_E_ARG, "msg_off not non-decreasing");
@@ -1491,13 +1515,23 @@ int edv_verify_batch(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msg
   if (!sigs || !pks || !msg_off || !accept) return set_err(EDV_E_ARG, "null pointer");
   if (!msgs && msg_off[n] != msg_off[0]) return set_err(EDV_E_ARG, "null msgs");
   int err;
-  bool uniform = false;
-  if ((err = check_offsets(msg_off, n, &uniform))) return err;
+  // A batch that runs as one shard (below 2 x min_shard()) has its offsets
+  // checked by the shard path itself, while its first copy is in flight (the
+  // scan of a C2 batch's 65,537 offsets is a few tens of microseconds of host
+  // time before the first byte would otherwise move); a small batch, or one
+  // that is split over devices (the split needs the scan), is checked here.
+  int uniform = -1;
+  if (msg_off[n] < msg_off[0]) return set_err(EDV_E_ARG, "msg_off not non-decreasing");
+  if (n < kDeferScanMin || n / min_shard() >= 2) {
+    bool u = false;
+    if ((err = check_offsets(msg_off, n, &u))) return err;
+    uniform = u ? 1 : 0;
+  }
   memset(accept, 0, n);  // fail closed: a call that fails part-way leaves rejections
   return for_each_shard(
       msg_off, n, device_mask,
       [&](DevCtx& c, uint64_t lo, uint64_t hi) { return run_shard(c, sigs, pks, msgs, msg_off, lo, hi, accept, uniform); },
-      uniform ? 1 : 0);
+      uniform);
 }
 
 int edv_verify_batch_async(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* msg_off,

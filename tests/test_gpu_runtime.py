@@ -166,6 +166,21 @@ def test_host_field_slices_path(n, slices):
                                                   views[2].ctypes.data, n, acc.ctypes.data, 0))
             assert np.array_equal(acc, want)
         pb.free()
+        # the same arrays pinned in reverse order (messages, offsets, keys, signatures):
+        # no single sigs | keys | offsets region, so three separate copies
+        pb = edv.PinnedBuffer(sum(p.nbytes for p in bufs) + 4 * 64 + n)
+        pos, views = 0, [None] * 4
+        for k in (3, 2, 1, 0):
+            v = pb.array[pos:pos + bufs[k].nbytes]
+            v[:] = bufs[k]
+            views[k] = v
+            pos += (bufs[k].nbytes + 63) // 64 * 64
+        acc = pb.array[pos:pos + n]
+        acc[:] = 7
+        edv._check(edv.lib().edv_verify_batch(views[0].ctypes.data, views[1].ctypes.data, views[3].ctypes.data,
+                                              views[2].ctypes.data, n, acc.ctypes.data, 0))
+        assert np.array_equal(acc, want)
+        pb.free()
     finally:
         edv.set_host_slices(0, 0)
 
