@@ -913,15 +913,17 @@ OffScan scan_offsets(const uint64_t* off, uint64_t lo, uint64_t hi) {
 // sub-batch's kernels take a whole batch's time (latency-bound lanes, DESIGN.md
 // section 3).  Splitting it by input field can: the two point sides need only
 // the signatures (R) and keys (A), 27 % of the bytes, and the hash side only
-// the messages (71 %) besides.  So: H2D of sigs, pks and offsets, then of the
-// messages in `slices` slices by request, on the copy stream; the point sides
-// (and the length buckets) start on stream hs[0] as soon as the first part is
-// in, while the messages still copy; the hash side of each slice on hs[1..3]
-// (in turn) as soon as its messages are in, so only the last slice's hash side
-// is left after the copy; the main kernel on hs[0] after all of them; then the
-// verdicts' D2H.  Length-bucketed shards (messages of several SHA-512 block
-// counts) hash in one piece after the whole copy: the bucket permutation
-// spans the shard.  Caller holds c.mu.
+// the messages (71 %) besides.  So: H2D of sigs, pks and offsets (one copy
+// when they are contiguous), then of the messages in `slices` slices by request,
+// on the copy stream; the point sides (and the length buckets) start on stream
+// hs[0] as soon as the first part is in, while the messages still copy; the
+// hash side of each slice as soon as its messages are in (one slice: in order
+// on hs[0]; several: on hs[1..3] in turn), so only the last slice's hash side
+// is left after the copy; the main kernel on hs[0] after all of them, writing
+// the verdicts straight into page-locked host memory.  Length-bucketed shards
+// (messages of several SHA-512 block counts) hash in one piece after the whole
+// copy: the bucket permutation spans the shard.  Anatomy of a C2 call:
+// DESIGN.md section 3, "The synchronous call".  Caller holds c.mu.
 // uniform: 1 / 0 = the offsets were checked and every message has (not) one
 // SHA-512 block count; -1 = not checked yet: the check runs here, on the host,
 // while the first copy (whose size depends on n only) is already on its way,
@@ -991,6 +993,14 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
   }
   HIPOK(hipEventRecord(c.part_copied[0], cp), "record");
   int err;
+  // The kernels write the verdicts straight into the page-locked host buffer
+  // (one 64-byte PCIe write per wave), so no D2H copy and its launch gap follow
+  // the main kernel (C2 pinned 1.075 -> 1.046 ms, with the in-stream hash side
+  // below 1.033-1.048 ms: profiles/r05/ab_sync_s4.jsonl).
+  void* zc = nullptr;
+  if (hipHostGetDevicePointer(&zc, h_acc, 0) == hipSuccess && zc) d_acc = static_cast<uint8_t*>(zc);
+  else (void)hipGetLastError();
+  const bool zc_acc = zc != nullptr;
   // the point sides first: they need only what has just been queued
   VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, mbase, d_acc, bucket);
   va.n = n;
@@ -1016,7 +1026,10 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
     }
   }
   for (int k = 0; k < K; k++) {
-    const hipStream_t hk = c.hs[1 + k % (kQ - 1)];
+    // one slice: the hash side in order behind the point sides on s0 (they are
+    // done long before the messages land), so main follows it in-stream with no
+    // cross-stream event between them
+    const hipStream_t hk = K == 1 ? s0 : c.hs[1 + k % (kQ - 1)];
     // requests [rb[k], rb[k+1]) of the shard: scratch slots and request index
     // both start at rb[k] (a bucketed shard is one slice, over the permutation)
     VerifyArgs vh = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, mbase, d_acc, bucket, rb[k]);
@@ -1029,9 +1042,10 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
     if ((err = launch_prep_sides(vh, hk))) return err;
     HIPOK(hipEventRecord(c.slice_hashed[k], hk), "record");
   }
-  for (int k = 0; k < K; k++) HIPOK(hipStreamWaitEvent(s0, c.slice_hashed[k], 0), "wait hash side");
+  if (K > 1)
+    for (int k = 0; k < K; k++) HIPOK(hipStreamWaitEvent(s0, c.slice_hashed[k], 0), "wait hash side");
   if ((err = launch_main(va, s0))) return err;
-  HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, s0), "d2h accept");
+  if (!zc_acc) HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, s0), "d2h accept");
   HIPOK(hipEventRecord(c.st_done, s0), "record scratch");
   HIPOK(hipStreamWaitEvent(c.stream, c.st_done, 0), "join");
   HIPOK(hipStreamSynchronize(s0), "stream sync");
