@@ -76,6 +76,10 @@ C3_DAMAGE_EVERY = 20      # 5 % invalid
 PEAK_INT32 = 256 * 64 * 2.4e9
 PEAK_VOP2 = 2 * PEAK_INT32
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
+PEAK_HBM = 8e12  # B/s, MI355X_MICROARCH.md "HBM"
+# the controlled Infinity-Cache run (tools/flush_probe.py):
+# main kernel time with every table line forced to DRAM between prep and main
+FLUSH_PROBE = os.path.join(ROOT, "profiles", "r05", "flush_probe_s1.jsonl")
 
 
 def w_blocks(m):
@@ -98,16 +102,14 @@ def kernel_source_hash():
     return h.hexdigest()
 
 
-# What the traffic figure is and why it stays: measured,
-# profiles/r03/pmc_extra_s10.json and bench_c3_full_s10.json.
-TRAFFIC_NOTE = ("L2-to-fabric bytes: the main kernel gathers one 160-B entry per window from each of two per-lane "
-                "1,440-B point tables the prep kernel wrote (~17.6 kB per verify; 2 x 128-B lines per entry), not "
-                "the 361 B of inputs. The counters cannot split Infinity-Cache hits from DRAM "
-                "(TCC_EA0_RDREQ_DRAM_sum == TCC_EA0_RDREQ_sum); at C2 the 189 MB of tables fit the 256 MiB "
-                "Infinity Cache, at 2^18 per launch (755 MB of tables, read from DRAM) the main kernel takes no "
-                "longer per verify, so the traffic is not what bounds it")
-
-
+# What the traffic figure is ("HBM traffic, calibrated"):
+# profiles/r05/gather_calibration_s1.json, flush_probe_s1.jsonl.
+TRAFFIC_NOTE = ("L2-to-fabric bytes, calibrated on known byte counts for this gather pattern "
+                "(tools/ubench_gather.hip: 128 B x the L2's 128-B fabric read requests = the bytes, 2 x FETCH_SIZE "
+                "agrees): the main kernel gathers one 160-B entry per window from each of two per-lane 1,440-B point "
+                "tables the prep kernel wrote, ~4.9x re-read within the launch and served on die (L2 misses, "
+                "Infinity-Cache hits; no gfx950 counter separates those from DRAM). What can reach DRAM is bounded "
+                "by the distinct bytes: inputs + prep's writes + main's first reads of them")
 def pmc_figures(kernels, batch, msg_len, kernel_ms):
     """Counter-derived figures for the verify path (`kernels`, summed) from the
     committed rocprofv3 PMC summary (tools/pmc_summary.py), only if it was
@@ -123,24 +125,44 @@ def pmc_figures(kernels, batch, msg_len, kernel_ms):
     if not all(ks):
         return None, "kernel not in PMC summary"
     out = {"traffic": sum(k.get("hbm_bytes_per_launch", 0.0) for k in ks),
-           "traffic_source": "%s: 2 x FETCH_SIZE + WRITE_SIZE per launch, prep + main (gfx950 correction; "
-                             "Infinity-Cache (MALL) hits included, so an upper bound on DRAM bytes)"
+           "traffic_source": "%s: fabric read bytes from the L2's request-size counters (128 x TCC_EA0_RDREQ_128B "
+                             "+ 64 x _64B + 32 x _32B; 2 x FETCH_SIZE agrees) + WRITE_SIZE, per launch, prep + main; "
+                             "Infinity-Cache (MALL) hits included, so an upper bound on DRAM bytes"
                              % os.path.relpath(PMC_SUMMARY, ROOT)}
     for key in ("dram_bytes_per_launch_bound", "dram_note"):
         if key in s:
             out[key] = s[key]
     out["traffic_per_verify_bytes"] = out["traffic"] / batch
+    prep, main = s["kernels"].get("edv_prep_kernel", {}), s["kernels"].get("edv_main_kernel", {})
+    if "read_bytes" in prep and "read_bytes" in main:
+        split = {"inputs_read_by_prep": prep["read_bytes"] / batch,
+                 "tables_and_digits_written_by_prep": prep["write_bytes"] / batch,
+                 "tables_gathered_by_main": main["read_bytes"] / batch}
+        out["traffic_split_per_verify_bytes"] = split
+        # distinct bytes: the inputs (algorithmic), what prep wrote, main's first read of the two tables
+        dram = (64 + 32 + msg_len + 8 + 1) + split["tables_and_digits_written_by_prep"] + 2 * 1440
+        out["dram_bytes_per_verify_upper_bound"] = dram
+        out["dram_upper_bound_note"] = ("every distinct byte crossing DRAM once each way (nothing kept in the 256 MiB "
+                                        "Infinity Cache from prep to main); the re-reads stay on die")
     out["traffic_note"] = TRAFFIC_NOTE
+    if os.path.exists(FLUSH_PROBE):
+        summ = [json.loads(ln) for ln in open(FLUSH_PROBE) if '"summary"' in ln]
+        if summ:
+            out["main_kernel_time_with_tables_forced_to_dram"] = {
+                "ratio": summ[-1]["main_flushed_over_plain"],
+                "source": os.path.relpath(FLUSH_PROBE, ROOT) + ": a 512 MiB read+rewrite between prep and main"}
     cs = [k["counters"] for k in ks]
     if all("SQ_INSTS_VALU" in c for c in cs):
         valu = sum(c["SQ_INSTS_VALU"] for c in cs)  # wave-instructions per launch pair
         lane_ops = valu * 64  # one lane-op per active lane per VALU wave-instruction
         out.update({
             "valu_insts_per_verify": valu * 64 / batch,
-            "valu_int64_insts_per_verify": sum(c.get("SQ_INSTS_VALU_INT64", 0.0) for c in cs) * 64 / batch,
-            "valu_int32_insts_per_verify": sum(c.get("SQ_INSTS_VALU_INT32", 0.0) for c in cs) * 64 / batch,
+
             "measured_valu_lane_ops_per_s": lane_ops / (kernel_ms * 1e-3),
             "measured_valu_frac_of_issue_peak": lane_ops / (kernel_ms * 1e-3) / PEAK_INT32,
+            **({"valu_int64_insts_per_verify": sum(c["SQ_INSTS_VALU_INT64"] for c in cs) * 64 / batch,
+                "valu_int32_insts_per_verify": sum(c["SQ_INSTS_VALU_INT32"] for c in cs) * 64 / batch}
+               if all("SQ_INSTS_VALU_INT64" in c and "SQ_INSTS_VALU_INT32" in c for c in cs) else {}),
             "per_kernel": {name: {"valu_insts_per_wave": k.get("valu_insts_per_wave"), "waves": k["counters"].get("SQ_WAVES"),
                                   "valu_busy": k.get("valu_busy"), "wave_cycle_split": k.get("wave_cycle_split"),
                                   "hbm_bytes_per_launch": k.get("hbm_bytes_per_launch"),
@@ -890,6 +912,8 @@ def main():
                               "kernel time); peak = 256 CU x 64 lanes x 2.4 GHz (4-cycle VOP3 issue)"}
     if pmc:
         roofline.update(pmc)
+        if "dram_bytes_per_verify_upper_bound" in pmc:
+            roofline["dram_frac_of_hbm_peak_upper_bound"] = pmc["dram_bytes_per_verify_upper_bound"] * value / PEAK_HBM
     if world > 1:
         one_gpu = n * args.steps / alone   # rank 0's shard, timed alone
         out_multi = {"per_gpu_verifies_per_s": value / world,
