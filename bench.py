@@ -90,16 +90,25 @@ def w_total(m):
     return 217600 + 5500 * w_blocks(m)
 
 
-def kernel_source_hash():
-    """SHA-256 over the HIP sources of libedv.so (ties a committed PMC summary to the code it measured)."""
+def device_code_hash(lib=None):
+    """SHA-256 of the gfx950 device code inside libedv.so (its .hip_fatbin ELF
+    section): ties a committed PMC summary to the kernels it measured; host-only
+    changes to the library leave it unchanged."""
     import hashlib
-    d = os.path.join(ROOT, "indy-plenum_amd", "csrc")
-    h = hashlib.sha256()
-    for f in sorted(os.listdir(d)):
-        if f.endswith((".hip", ".h")):
-            h.update(f.encode())
-            h.update(open(os.path.join(d, f), "rb").read())
-    return h.hexdigest()
+    import struct
+    path = lib or os.path.join(ROOT, "indy-plenum_amd", "libedv.so")
+    b = open(path, "rb").read()
+    shoff = struct.unpack_from("<Q", b, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+
+    def sh(i):
+        return struct.unpack_from("<IIQQQQ", b, shoff + i * shentsize)
+    names = sh(shstrndx)[4]
+    for i in range(shnum):
+        nm, _typ, _fl, _addr, off, size = sh(i)
+        if b[names + nm:b.index(b"\0", names + nm)] == b".hip_fatbin":
+            return hashlib.sha256(b[off:off + size]).hexdigest()
+    raise ValueError("no .hip_fatbin section in %s" % path)
 
 
 # What the traffic figure is (DESIGN.md section 3, "HBM traffic, calibrated"):
@@ -119,8 +128,8 @@ def pmc_figures(kernels, batch, msg_len, kernel_ms):
         return None, "no PMC summary for this shape"
     with open(PMC_SUMMARY) as f:
         s = json.load(f)
-    if s.get("kernel_source_sha256") != kernel_source_hash():
-        return None, "PMC summary is stale (kernel sources changed since it was measured)"
+    if s.get("device_code_sha256") != device_code_hash():
+        return None, "PMC summary is stale (the library's device code changed since it was measured)"
     ks = [s["kernels"].get(k) for k in kernels]
     if not all(ks):
         return None, "kernel not in PMC summary"

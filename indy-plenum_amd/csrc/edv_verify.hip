@@ -1825,7 +1825,12 @@ int edv_profile_batch_dev_flush(const uint8_t* d_sigs, const uint8_t* d_pks, con
   va.n = n;
   uint32_t* hist = bucket_ctr(c->st, 0);
   const unsigned blocks = unsigned((n + kBlock - 1) / kBlock);
-  DevBuf flush;
+  // the flush buffer lives for this call only (DevBuf keeps its memory; this frees it)
+  struct FlushBuf : DevBuf {
+    ~FlushBuf() {
+      if (p) (void)hipFree(p);
+    }
+  } flush;
   flush_bytes &= ~uint64_t(15);
   if (flush_bytes && flush.ensure(flush_bytes)) return EDV_E_OOM;
   if (flush_bytes) HIPOK(hipMemsetAsync(flush.p, 0, flush_bytes, c->stream), "memset flush");

@@ -593,7 +593,7 @@ def test_bench_default_line_contract():
     assert rf["kernel_ms"] <= line["ms_per_step"] * 1.05
     with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                            "pmc_latest.json")) as f:
-        pmc_matches = json.load(f).get("kernel_source_sha256") == bench.kernel_source_hash()
+        pmc_matches = json.load(f).get("device_code_sha256") == bench.device_code_hash()
     assert (rf["traffic"] is not None) == pmc_matches
     cb = line["cpu_baseline"]
     assert cb["kind"] in ("reference", "port") and cb["value"] > 0 and cb["cores"] >= 1 and cb["sample"]

@@ -21,9 +21,9 @@ instruction); SQ_ACTIVE_INST_VALU counts them in quad-cycles; GRBM_GUI_ACTIVE
 is summed over the 8 XCDs (MI355X_MICROARCH.md "DVFS give-back"), so the
 kernel's GPU-busy cycles are GRBM_GUI_ACTIVE / 8.
 
-The summary records the SHA-256 of the kernel sources it was measured on
-(bench.kernel_source_hash); bench.py reports its figures only while the
-sources still hash the same.
+The summary records the SHA-256 of the device code it was measured on
+(bench.device_code_hash: the .hip_fatbin section of libedv.so); bench.py
+reports its figures only while the library's device code hashes the same.
 """
 import collections
 import csv
@@ -33,7 +33,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bench import kernel_source_hash  # noqa: E402
+from bench import device_code_hash  # noqa: E402
 
 N_SIMD = 256 * 4
 
@@ -59,7 +59,7 @@ def summarise(root):
     out = {"source": "rocprofv3 --pmc, one counter group per pass, over bench.py --steps 6 --warmup 2",
            "correction": "read_bytes = 2 * FETCH_SIZE_KB * 1024 (gfx950), write_bytes = WRITE_SIZE_KB * 1024; "
                          "MALL (Infinity Cache) hits are included",
-           "kernel_source_sha256": kernel_source_hash(),
+           "device_code_sha256": device_code_hash(),
            "kernels": {}}
     for k, cs in sorted(acc.items()):
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
