@@ -21,6 +21,7 @@ constexpr int kAWords = kAEntries * kEntryWords;  // per-signature table (9 entr
 constexpr int kDigWords = 8 + 8 + kBDigits + 1;
 constexpr int kDigB = 16, kDigNwin = 16 + kBDigits;
 constexpr uint64_t kChunkDefault = uint64_t(1) << 18;  // signatures per prep/main launch pair
+constexpr int kBuckets = 64;  // SHA-512 length buckets (block counts 0..62, 63 = 63 or more)
 
 // Per-chunk state handed from the prep kernel to the main kernel, SoA so every
 // wave-wide load/store touches 64 consecutive words:

@@ -185,6 +185,41 @@ def test_host_field_slices_path(n, slices):
         edv.set_host_slices(0, 0)
 
 
+@pytest.mark.parametrize("slices", [1, 2])
+def test_host_field_path_empty_messages(slices):
+    """A batch whose messages are all empty (Ed25519 over zero bytes: no message
+    copy at all on the field path, SHA-512 of R || A alone), 10 % damaged, from
+    pageable and pinned buffers; verdicts equal libsodium's."""
+    n = 3000
+    rng = np.random.default_rng(0xE0 + slices)
+    seeds = rng.integers(0, 256, size=32 * n, dtype=np.uint8)
+    off = np.zeros(n + 1, np.uint64)
+    pks, sigs = edv.sign_arrays(seeds, b"", off)
+    sigs = sigs.copy()
+    sigs[64 * np.arange(0, n, 10) + 40] ^= 1          # every tenth S damaged
+    msgs = np.zeros(16, np.uint8)
+    want = checker(sigs, pks, msgs, off)
+    assert want.sum() == n - len(range(0, n, 10))
+    edv.set_host_slices(0, slices)
+    try:
+        assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off), want)
+        pb = edv.PinnedBuffer(sigs.nbytes + pks.nbytes + off.nbytes + n + 4 * 64)
+        pos, views = 0, []
+        for a in (sigs, pks, off.view(np.uint8)):
+            v = pb.array[pos:pos + a.nbytes]
+            v[:] = a
+            views.append(v)
+            pos += (a.nbytes + 63) // 64 * 64
+        acc = pb.array[pos:pos + n]
+        acc[:] = 7
+        edv._check(edv.lib().edv_verify_batch(views[0].ctypes.data, views[1].ctypes.data, msgs.ctypes.data,
+                                              views[2].ctypes.data, n, acc.ctypes.data, 0))
+        assert np.array_equal(acc, want)
+        pb.free()
+    finally:
+        edv.set_host_slices(0, 0)
+
+
 def test_host_field_path_varied_lengths_one_slice():
     """Messages of several SHA-512 block counts (C4 lengths) on the field path:
     the shard is length-bucketed, so its hash side runs in one piece after the
