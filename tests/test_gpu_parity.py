@@ -165,6 +165,35 @@ def test_fuzzed_damage_vs_libsodium():
     assert 0.4 < out["libsodium_rejected"] / 65536 < 0.8
 
 
+def test_bench_corpora_vs_libsodium_live():
+    """The bench's own generators (tools/parity_live_sodium.py: C3's 256-B
+    requests with four damage kinds, C4's 200..4,096-B requests with seven,
+    and the fuzz corpus through the synchronous host path in one-slice and
+    four-slice calls), verified on the GPU and by libsodium 1.0.18 itself on the
+    host, every verdict compared: the bench's corpora are checked against
+    libsodium here, not only by construction."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import parity_live_sodium as pl
+    if orc.sodium_batch() is None:
+        pytest.skip("libsodium batch harness absent")
+    c3 = pl.run("C3", 1 << 20, damage_every=20, damage_kinds=4)
+    c4 = pl.run("C4", 1 << 18, seed=0xC4C4, var_range=(200, 4096), damage_every=20, damage_kinds=7)
+    assert c3["mismatches"] == 0 and c3["libsodium_rejected"] == len(range(0, 1 << 20, 20)), c3
+    assert c4["mismatches"] == 0 and c4["libsodium_rejected"] > 0, c4
+    saved = os.environ.get("FUZZ_SLICE")
+    try:
+        for sl in (1 << 16, 1 << 18):       # one message slice, four
+            os.environ["FUZZ_SLICE"] = str(sl)
+            out = pl.fuzz(1 << 18, seed=0xF2 + sl)
+            assert out["requests"] == 1 << 18 and out["mismatches"] == 0, out
+    finally:
+        if saved is None:
+            os.environ.pop("FUZZ_SLICE", None)
+        else:
+            os.environ["FUZZ_SLICE"] = saved
+
+
 def test_full_size_c2_properties():
     """BASELINE configs[1] size (65,536 x 256 B, distinct signers): all valid
     accept; every kind of single-bit/malleation damage rejects exactly where applied."""
