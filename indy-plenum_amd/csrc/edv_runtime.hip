@@ -663,9 +663,10 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
   // (always so once staged; so for a caller that packs a batch into one
   // pinned buffer) go in ONE copy into a device block of the same layout: each
   // separate copy costs the DMA engine a gap (~12 us each, trace_sync).
-  const uint64_t gp = uint64_t(src_p - src_s), go = uint64_t(src_o - src_s), span = go + 8 * (n + 1);
-  if (src_p >= src_s + 64 * n && src_o >= src_p + 32 * n && span <= 104 * n + 8 + 4096 && gp % 16 == 0 &&
-      go % 8 == 0) {
+  const uintptr_t as = reinterpret_cast<uintptr_t>(src_s), ap = reinterpret_cast<uintptr_t>(src_p),
+                  ao = reinterpret_cast<uintptr_t>(src_o);
+  const uint64_t gp = ap - as, go = ao - as, span = go + 8 * (n + 1);
+  if (ap >= as + 64 * n && ao >= ap + 32 * n && span <= 104 * n + 8 + 4096 && gp % 16 == 0 && go % 8 == 0) {
     if (c.fblob.ensure(span)) return EDV_E_OOM;
     uint8_t* blob = static_cast<uint8_t*>(c.fblob.p);
     d_sigs = blob;
@@ -773,12 +774,11 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
               uint64_t hi, uint8_t* accept, int uniform) {
   const uint64_t n = hi - lo;
   if (n == 0) return 0;
-  // A shard that fits one chunk is one sub-batch on one stream: split 2 or 4
-  // ways at 64k it measured 1.6x / 1.9x slower (tools/e2e_probe.py,
-  // profiles/r02/e2e_probe_s4.json), as a 16k sub-batch still takes a whole
-  // batch's latency at one wave per SIMD.  A larger shard alternates two
-  // streams of half-chunk sub-batches, so the H2D copy of one overlaps the
-  // kernels of the other.  EDV_HOST_STREAMS (1..4) overrides, for measurement.
+  // A shard that fits one chunk is one sub-batch (the field path): split 2 or
+  // 4 ways at 64k it measured 1.6x / 1.9x slower (profiles/r02/e2e_probe_s4.json),
+  // as a 16k sub-batch still takes a whole batch's latency at one wave per
+  // SIMD.  A larger shard alternates two streams of half-chunk sub-batches, so
+  // the H2D copy of one overlaps the kernels of the other.
   const int Q = (n > c.chunk && c.chunk >= 2 * uint64_t(kBlock)) ? 2 : 1;
   const uint64_t pmax = c.chunk / Q;
   uint64_t P = (n + Q - 1) / Q;

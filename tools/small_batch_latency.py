@@ -1,10 +1,8 @@
 """Latency of Node-sized batches (1 .. 4,096 requests of 256 B) on one MI355X
 from pinned host buffers: a synchronous edv_verify_batch call, and an
-edv_verify_batch_async submission + edv_wait_async, each with the DMA copies
-(default) and zero-copy (EDV_ZERO_COPY=1: the kernels read the pinned inputs
-and write the pinned verdicts over the link).  Median of R calls; verdicts
-checked.  Measurement only.(EDV_ZERO_COPY was removed from the library after this measurement,
-profiles/r04/small_batch_latency_s2.jsonl; with HEAD both rows take the copy path.)
+edv_verify_batch_async submission + edv_wait_async.  Median of R calls;
+verdicts checked.  Measurement only.  (Round 4 also timed a zero-copy input
+mode, profiles/r04/small_batch_latency_s2.jsonl; it was removed.)
 """
 import json
 import os
@@ -48,12 +46,7 @@ def med(f):
 
 for n in sizes:
     o = po[:n + 1]
-    for zc in (False, True):
-        if zc:
-            os.environ["EDV_ZERO_COPY"] = "1"
-        else:
-            os.environ.pop("EDV_ZERO_COPY", None)
-
+    if True:
         def sync():
             edv._check(lib.edv_verify_batch(ps.ctypes.data, pp.ctypes.data, pm.ctypes.data, o.ctypes.data, n,
                                             pa.ctypes.data, 1))
@@ -67,5 +60,5 @@ for n in sizes:
         pa[:] = 2
         asyn()
         ok_a = bool(np.array_equal(pa[:n], want[:n]))
-        rec = {"n": n, "zero_copy": zc, "sync_ms": med(sync), "async_ms": med(asyn), "ok": ok_s and ok_a}
+        rec = {"n": n, "sync_ms": med(sync), "async_ms": med(asyn), "ok": ok_s and ok_a}
         print(json.dumps(rec), flush=True)

@@ -3,9 +3,9 @@
   split:  for tools/ab_split.py (MODES=split) -- how much of each hash-side
           prep launch (edv_prep_kernel, grid n) ran while a main kernel was
           running, and the per-class kernel durations
-  fields: for tools/e2e_fields.py -- per synchronous call on the field-ordered
-          path, how long the point-side prep launch (grid 2n) ran before the
-          message copy finished
+  fields: per synchronous call on the field-ordered path (a trace of
+          synchronous calls, e.g. tools/trace_sync.py's), how long the
+          point-side prep launch (grid 2n) ran before the message copy finished
 
   python tools/trace_split.py split|fields <trace dir> [n=65536]
 Measurement only."""
