@@ -969,11 +969,18 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
     HIPOK(hipEventRecord(s.copied, c.hcp), "record");
     HIPOK(hipStreamWaitEvent(c.hac, s.copied, 0), "wait copy");
   }
+  uint8_t* h_acc = s.acc_pinned ? accept : static_cast<uint8_t*>(s.acc_host.p);
+  // verdicts written by the kernels straight into page-locked host memory, as
+  // in the synchronous path: no D2H between this batch's main kernel and the
+  // next batch's prep on the stream (a C2 stream of batches 0.945 -> 0.965x
+  // device-resident, profiles/r05/ab_async_s7.jsonl)
+  void* zc = nullptr;
+  if (hipHostGetDevicePointer(&zc, h_acc, 0) == hipSuccess && zc) d_acc = static_cast<uint8_t*>(zc);
+  else (void)hipGetLastError();
   if ((err = own ? launch_own(c, s.cb, kSmallAsync, d_sigs, d_pks, d_msgs, d_off, mbase, n, d_acc, ks, lflags)
                  : launch(c, d_sigs, d_pks, d_msgs, d_off, mbase, n, d_acc, ks, lflags)))
     return err;
-  uint8_t* h_acc = s.acc_pinned ? accept : static_cast<uint8_t*>(s.acc_host.p);
-  HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, ks), "d2h accept");
+  if (!zc) HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, ks), "d2h accept");
   if (digests) {
     // Request.getDigest of requests whose signing bytes ARE the message (the
     // caller decides which): SHA-256 of the same resident message bytes

@@ -1,28 +1,30 @@
 """Back-to-back edv_verify_batch_async from pinned host buffers (the product's
-stream-of-batches boundary) at C2 (65,536 x 256 B) and C4 (65,536 x 200..4,096
-B, 5 % invalid): a stream of K batches, waiting one batch behind, per-batch
-time as the median of R streams; EDV_ASYNC_SPLIT unset (auto: the split
-pipeline from a mean of 6 SHA-512 blocks), 0 (off) and 1 (on); verdicts checked
-on every stream.  Also the device-resident sequential step for reference.
-Measurement only.(EDV_ASYNC_SPLIT was removed from the library after this measurement,
-profiles/r04/async_stream_s13.jsonl; with HEAD all three rows take the ordinary path.)
+stream-of-batches boundary) at C2 (65,536 x 256 B) and C4 (65,536 x
+200..4,096 B, 5 % invalid): a stream of K batches waiting one batch behind,
+per-batch time as the median of R streams, next to the device-resident
+sequential step; verdicts checked on every stream.  With library paths as
+arguments, each .so (EDV_LIB) runs in its own process, in the order given
+(A B A B interleaves them).  Measurement only.
+
+  python tools/async_stream.py [lib.so ...]
 """
 import json
 import os
-import statistics
+import subprocess
 import sys
-import time
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r"""
+import json, os, statistics, sys, time
 import numpy as np
-
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from indy_plenum_amd import edv, workload  # noqa: E402
-
+sys.path.insert(0, os.environ["ROOT"])
+from indy_plenum_amd import edv, workload
 K, R = int(os.environ.get("K", 32)), int(os.environ.get("R", 5))
 dev = 0
 s = edv.stream(dev)
 cfgs = {"C2": dict(), "C4": dict(seed=0xC4C4, var_range=(200, 4096), damage_every=20, damage_kinds=7)}
-for name, kw in cfgs.items():
+for name in os.environ.get("CFGS", "C2,C4").split(","):
+    kw = cfgs[name]
     b = workload.DeviceBatch(65536, device=dev, keep_host=True, **kw)
     sigs, pks, msgs, off = b.host_copy()
     want = b.expected()
@@ -41,9 +43,10 @@ for name, kw in cfgs.items():
     reps = []
     for _ in range(R):
         t0 = time.perf_counter()
-        b.verify(stream=s)
+        for _ in range(K):
+            b.verify(stream=s)
         edv.sync(dev)
-        reps.append(time.perf_counter() - t0)
+        reps.append((time.perf_counter() - t0) / K)
     dev_ms = 1e3 * statistics.median(reps)
 
     def stream():
@@ -54,22 +57,23 @@ for name, kw in cfgs.items():
                 edv.wait_async(prev, device=dev)
             prev = t
         edv.wait_async(prev, device=dev)
-    for mode in (None, "0", "1"):
-        if mode is None:
-            os.environ.pop("EDV_ASYNC_SPLIT", None)
-        else:
-            os.environ["EDV_ASYNC_SPLIT"] = mode
-        for a in accs:
-            a[:] = 7
+    for a in accs:
+        a[:] = 7
+    stream()
+    ok = all(bool(np.array_equal(a, want)) for a in accs)
+    ts = []
+    for _ in range(R):
+        t0 = time.perf_counter()
         stream()
-        ok = all(bool(np.array_equal(a, want)) for a in accs)
-        ts = []
-        for _ in range(R):
-            t0 = time.perf_counter()
-            stream()
-            ts.append((time.perf_counter() - t0) / K)
-        ms = 1e3 * statistics.median(ts)
-        print(json.dumps({"config": name, "async_split": mode or "auto", "ms_per_batch": ms,
-                          "verifies_per_s": n / (ms * 1e-3), "device_resident_seq_ms": dev_ms,
-                          "verdicts_ok": ok}), flush=True)
+        ts.append((time.perf_counter() - t0) / K)
+    ms = 1e3 * statistics.median(ts)
+    print(json.dumps({"lib": os.path.basename(os.environ.get("EDV_LIB", "libedv.so")), "config": name,
+                      "ms_per_batch": ms, "verifies_per_s": n / (ms * 1e-3), "device_resident_seq_ms": dev_ms,
+                      "async_vs_device_resident": dev_ms / ms, "verdicts_ok": ok}), flush=True)
     pb.free()
+"""
+libs = sys.argv[1:] or [os.path.join(ROOT, "indy-plenum_amd", "libedv.so")]
+for lib in libs:
+    env = dict(os.environ, EDV_LIB=os.path.abspath(lib), ROOT=ROOT)
+    r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=600)
+    print(r.stdout.strip() if r.returncode == 0 else json.dumps({"lib": lib, "error": r.stderr[-800:]}), flush=True)
