@@ -8,6 +8,7 @@
 #           (timing, then PMC passes per dispatch)
 #   prof    rocprofv3 --kernel-trace --stats over the C2 bench (no extra legs)
 #   pmc     rocprofv3 --pmc passes over the C2 bench + summary (profiles/pmc_latest.json)
+#   lds     one --pmc pass of LDS / wait counters over the C2 bench (where the main kernel waits)
 #   extra   $EXTRA (a command line)
 # Every GPU step has its own time limit; the chain stops at the first failure.
 # Outputs land in gpurun_out/r05/<TAG>/.
@@ -94,6 +95,13 @@ if has pmc; then
       || { echo "pmc pass $i failed"; tail -20 $O/pmc_p$i.log; exit 1; }
   done
   python3 tools/pmc_summary.py $O/pmc $O/pmc_summary.json > /dev/null && echo "pmc summary written"
+fi
+if has lds; then
+  log lds
+  (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS \
+    SQ_LDS_BANK_CONFLICT SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_INSTS_LDS -d $O/lds -o run --output-format csv \
+    -- python3 $R/bench.py --steps 6 --warmup 1 $QUIET > $O/lds.log 2>&1) || fail lds $O/lds.log
+  echo "lds pass done"
 fi
 if has extra; then
   log extra
