@@ -2,7 +2,8 @@
 stream-of-batches boundary) at C2 (65,536 x 256 B) and C4 (65,536 x
 200..4,096 B, 5 % invalid): a stream of K batches waiting one batch behind,
 per-batch time as the median of R streams, next to the device-resident
-sequential step; verdicts checked on every stream.  With library paths as
+sequential step; verdicts checked on every stream (PAGEABLE=1: from the
+caller's pageable numpy arrays instead).  With library paths as
 arguments, each .so (EDV_LIB) runs in its own process, in the order given
 (A B A B interleaves them).  Measurement only.
 
@@ -40,6 +41,10 @@ for name in os.environ.get("CFGS", "C2,C4").split(","):
     ps, pp, po, pm = views
     po = po.view(np.uint64)
     accs = (pb.array[pos:pos + n], pb.array[pos + n:pos + 2 * n])
+    pageable = os.environ.get("PAGEABLE") == "1"
+    if pageable:  # the caller's own (pageable) numpy buffers: staged by the library
+        ps, pp, pm, po = sigs, pks, msgs, off
+        accs = (np.zeros(n, np.uint8), np.zeros(n, np.uint8))
     reps = []
     for _ in range(R):
         t0 = time.perf_counter()
@@ -68,6 +73,7 @@ for name in os.environ.get("CFGS", "C2,C4").split(","):
         ts.append((time.perf_counter() - t0) / K)
     ms = 1e3 * statistics.median(ts)
     print(json.dumps({"lib": os.path.basename(os.environ.get("EDV_LIB", "libedv.so")), "config": name,
+                      "inputs": "pageable" if pageable else "pinned",
                       "ms_per_batch": ms, "verifies_per_s": n / (ms * 1e-3), "device_resident_seq_ms": dev_ms,
                       "async_vs_device_resident": dev_ms / ms, "verdicts_ok": ok}), flush=True)
     pb.free()
