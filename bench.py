@@ -77,9 +77,11 @@ PEAK_INT32 = 256 * 64 * 2.4e9
 PEAK_VOP2 = 2 * PEAK_INT32
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
 PEAK_HBM = 8e12  # B/s, MI355X_MICROARCH.md "HBM"
+# the R side's [S]B gathers per verify: kBTables (12) entries of 128 B (edv_verify_core.h)
+SB_GATHER_BYTES = 12 * 128
 # the controlled Infinity-Cache run (tools/flush_probe.py):
 # main kernel time with every table line forced to DRAM between prep and main
-FLUSH_PROBE = os.path.join(ROOT, "profiles", "r05", "flush_probe_s1.jsonl")
+FLUSH_PROBE = os.path.join(ROOT, "profiles", "r05", "flush_probe_s15.jsonl")
 
 
 def w_blocks(m):
@@ -117,8 +119,9 @@ TRAFFIC_NOTE = ("L2-to-fabric bytes, calibrated on known byte counts for this ga
                 "(tools/ubench_gather.hip: 128 B x the L2's 128-B fabric read requests = the bytes, 2 x FETCH_SIZE "
                 "agrees): the main kernel gathers one 160-B entry per window from each of two per-lane 1,440-B point "
                 "tables the prep kernel wrote, ~4.9x re-read within the launch and served on die (L2 misses, "
-                "Infinity-Cache hits; no gfx950 counter separates those from DRAM). What can reach DRAM is bounded "
-                "by the distinct bytes: inputs + prep's writes + main's first reads of them")
+                "Infinity-Cache hits; no gfx950 counter separates those from DRAM); the prep kernel's R side gathers "
+                "12 x 128 B per verify from the 3 GiB shared [S]B tables (random lines: DRAM). What can reach DRAM "
+                "is bounded by the distinct bytes: prep's reads + prep's writes + main's first reads of the tables")
 def pmc_figures(kernels, batch, msg_len, kernel_ms):
     """Counter-derived figures for the verify path (`kernels`, summed) from the
     committed rocprofv3 PMC summary (tools/pmc_summary.py), only if it was
@@ -144,12 +147,14 @@ def pmc_figures(kernels, batch, msg_len, kernel_ms):
     out["traffic_per_verify_bytes"] = out["traffic"] / batch
     prep, main = s["kernels"].get("edv_prep_kernel", {}), s["kernels"].get("edv_main_kernel", {})
     if "read_bytes" in prep and "read_bytes" in main:
-        split = {"inputs_read_by_prep": prep["read_bytes"] / batch,
+        split = {"inputs_and_sb_tables_read_by_prep": prep["read_bytes"] / batch,
+                 "sb_table_gathers_algorithmic": SB_GATHER_BYTES,
                  "tables_and_digits_written_by_prep": prep["write_bytes"] / batch,
                  "tables_gathered_by_main": main["read_bytes"] / batch}
         out["traffic_split_per_verify_bytes"] = split
-        # distinct bytes: the inputs (algorithmic), what prep wrote, main's first read of the two tables
-        dram = (64 + 32 + msg_len + 8 + 1) + split["tables_and_digits_written_by_prep"] + 2 * 1440
+        # distinct bytes: what prep read (inputs, [S]B entries), what it wrote,
+        # main's first read of the two per-lane tables
+        dram = split["inputs_and_sb_tables_read_by_prep"] + split["tables_and_digits_written_by_prep"] + 2 * 1440
         out["dram_bytes_per_verify_upper_bound"] = dram
         out["dram_upper_bound_note"] = ("every distinct byte crossing DRAM once each way (nothing kept in the 256 MiB "
                                         "Infinity Cache from prep to main); the re-reads stay on die")

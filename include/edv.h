@@ -248,7 +248,7 @@ int edv_device_count(void);
  * shard; the Node's asynchronous path asks it for the device of each
  * submission (edv_verify_batch_async takes the device explicitly).
  * edv_pick_device returns that device's index (or a negative EDV_E_* code);
- * edv_context_count: devices whose context (streams, scratch, B table) exists.
+ * edv_context_count: devices whose context (streams, scratch, [S]B tables) exists.
  * Reference: the per-request call being placed, nacl_wrappers.py:232-242, made
  * per prod (plenum/server/node.py:1026-1049, stp_core/config.py:28).
  */

@@ -21,23 +21,28 @@ struct HostATab {
   void stage(int e) { staged = e; }
   ge_cached fetch() const { return t[staged]; }
 };
+// The R side's view of the [S]B tables: each entry computed when asked for, by
+// the device table's own btab_entry (the 16 x 32,769 entries would take a
+// minute to build on one core; a verify needs 16 of them).
 struct HostBTab {
-  std::vector<int32_t> w;
-  HostBTab() : w(kBTables * kBEntries * kBStride) {
-    for (int t = 0; t < kBTables; t++) {
-      const ge_p3 base = base_point(t * kBSplit);
-      for (int j = 0; j < kBEntries; j++) btab_entry(w.data() + (t * kBEntries + j) * kBStride, j, base);
-    }
+  ge_p3 base[kBTables];
+  HostBTab() {
+    for (int t = 0; t < kBTables; t++) base[t] = base_point(t * kBBits);
   }
-  ge_precomp entry(int t, int j) const { return precomp_from_words(w.data() + (t * kBEntries + j) * kBStride); }
+  ge_precomp entry(int t, int j) const {
+    int32_t w[kBStride];
+    btab_entry(w, j, base[t]);
+    return precomp_from_words(w);
+  }
 };
-// the main loop's staged view of the B tables
 struct HostBStage {
   const HostBTab& b;
-  int j[kBTables] = {0, 0};
-  void issue() {}
-  void stage(int t, int e) { j[t] = e; }
-  ge_precomp fetch(int t) const { return b.entry(t, j[t]); }
+  int t = 0, j = 0;
+  ge_cached stash;
+  void stage(int tt, int jj) { t = tt; j = jj; }
+  ge_precomp fetch() const { return b.entry(t, j); }
+  void put(const ge_cached& c) { stash = c; }
+  ge_cached get() const { return stash; }
 };
 struct HostComb {
   std::vector<int32_t> w;
@@ -123,11 +128,31 @@ int hc_sha256_batch(const uint8_t* msgs, const uint64_t* off, uint64_t n, uint8_
   }
   return 0;
 }
-void hc_btab(int32_t* out) { memcpy(out, btab().w.data(), sizeof(int32_t) * kBEntries * kBStride); }
-// table t (0: j B, 1: j 2^kBSplit B)
-int hc_btab_table(int t, int32_t* out) {
+// entries js[0..nj) of table t (j x 2^(kBBits t) B), kBStride words each
+int hc_btab_entries_of(int t, const int32_t* js, int nj, int32_t* out) {
   if (t < 0 || t >= kBTables) return -1;
-  memcpy(out, btab().w.data() + size_t(t) * kBEntries * kBStride, sizeof(int32_t) * kBEntries * kBStride);
+  for (int k = 0; k < nj; k++) {
+    if (js[k] < 0 || js[k] >= kBEntries) return -1;
+    btab_entry(out + size_t(k) * kBStride, js[k], btab().base[t]);
+  }
+  return 0;
+}
+// the R side's Q = [S]B - R, encoded (0), or -1 if R is rejected
+int hc_rside_point(const uint8_t* R32, const uint8_t* S32, uint8_t* out32) {
+  struct Keep {  // keeps entry 1 of the table: Q itself
+    ge_cached q;
+    void store(int e, const ge_cached& c) { if (e == 1) q = c; }
+  } tab;
+  uint32_t R[8], S[8], o[8];
+  load_words(R, R32, 8);
+  load_words(S, S32, 8);
+  HostBStage bs{btab()};
+  if (!prep_rpoint(R, S, tab, bs)) return -1;
+  // cached (Y+X, Y-X, Z, 2dT) -> (X : Y : Z)
+  const fe two_y = fe_carry32(fe_add(tab.q.YpX, tab.q.YmX)), two_x = fe_carry32(fe_sub(tab.q.YpX, tab.q.YmX));
+  ge_p2 p{two_x, two_y, fe_carry32(fe_add(tab.q.Z, tab.q.Z))};
+  ge_p2_tobytes(o, p);
+  store_words(out32, o, 8);
   return 0;
 }
 // the lattice reduction of the prep kernel: (a, u, neg) for h (32-byte scalars)
@@ -140,16 +165,10 @@ int hc_half_scalars(const uint8_t* h32, uint8_t* a32, uint8_t* u32) {
   store_words(u32, u, 8);
   return neg ? 1 : 0;
 }
-// the walk's layout constants: kAWin, kAEntries, kBBits, kBSplit, kBDigits, kBEvery, kBMinWindows
-void hc_layout(int32_t* out7) {
-  const int32_t v[7] = {kAWin, kAEntries, kBBits, kBSplit, kBDigits, kBEvery, kBMinWindows};
-  memcpy(out7, v, sizeof v);
-}
-// B-scalar digit pairs of s (kBDigits words)
-void hc_recode_bscalar(const uint8_t* s32, uint32_t* out9) {
-  uint32_t s[8];
-  load_words(s, s32, 8);
-  recode_bscalar(out9, s);
+// the walk's layout constants: kAWin, kAEntries, kBBits, kBTables
+void hc_layout(int32_t* out4) {
+  const int32_t v[4] = {kAWin, kAEntries, kBBits, kBTables};
+  memcpy(out4, v, sizeof v);
 }
 int hc_btab_entries() { return kBEntries; }
 // the asynchronous path's ticket ledger (edv_ledger.h): issue n tickets, fail
@@ -163,16 +182,13 @@ void hc_ledger(int64_t n, const int64_t* failed, int nf, const int64_t* queries,
 // windows the packed radix-2^kAWin digits need (the prep kernel's per-lane count)
 int hc_digits_windows(const uint32_t* d8) { return digits5_windows(d8); }
 // packed signed digits of a 32-byte scalar at radix 2^bits: 4 (64 digits: the main
-// loop's windows at kAWin = 4), 5 (51 digits), 8 -> recode8 (signer), 15 / 16 -> the
-// generic recoder (17 / 16 digits)
+// loop's windows at kAWin = 4), 5 (51 digits), 8 -> recode8 (signer)
 int hc_recode(const uint8_t* in32, int bits, uint32_t* out8) {
   uint32_t w[8];
   load_words(w, in32, 8);
   if (bits == 4) recode4(out8, w);
   else if (bits == 5) recode5_fixed(out8, w);
   else if (bits == 8) recode8(out8, w);
-  else if (bits == 15) recode15(out8, w);
-  else if (bits == 16) recode16(out8, w);
   else return -1;
   return 0;
 }

@@ -17,18 +17,18 @@ namespace edv {
 constexpr int kBlock = 256;
 constexpr int kEntryWords = 40;           // cached point = 4 x 10 limbs, 160 B
 constexpr int kAWords = kAEntries * kEntryWords;  // per-signature table (9 entries: 360 words = 1,440 B)
-// dig words per signature: da (8), db (8), B digit pairs (kBDigits), window count (1)
-constexpr int kDigWords = 8 + 8 + kBDigits + 1;
-constexpr int kDigB = 16, kDigNwin = 16 + kBDigits;
+// dig words per signature: da (8), db (8), window count and sign (1)
+constexpr int kDigWords = 8 + 8 + 1;
+constexpr int kDigNwin = 16;
 constexpr uint64_t kChunkDefault = uint64_t(1) << 18;  // signatures per prep/main launch pair
 constexpr int kBuckets = 64;  // SHA-512 length buckets (block counts 0..62, 63 = 63 or more)
 
 // Per-chunk state handed from the prep kernel to the main kernel, SoA so every
 // wave-wide load/store touches 64 consecutive words:
 //   atab[kAWords * i + w]  word w of signature i's 0..kAEntries-1 x (-A) table
-//   rtab[kAWords * i + w]  the same for its 0..kAEntries-1 x (-+R) table
+//   rtab[kAWords * i + w]  the same for its 0..kAEntries-1 x ([S]B - R) table
 //   dig[w * cap + i]   w 0..7: packed radix-2^kAWin digits of a, 8..15: of |b|,
-//                      16..: kBDigits B-scalar digit pairs, last: windows needed
+//                      16: windows needed | (b < 0) << 8
 //   alive[k cap + i]   1 if prep side k (0 hash, 1 A, 2 R) passed for slot i (the
 //                      main kernel skips lanes where any side failed)
 struct ChunkState {
@@ -50,7 +50,7 @@ struct VerifyArgs {
   uint64_t n;             // signatures in this chunk
   uint8_t* accept;        // indexed by global signature index
   ChunkState st;
-  const int32_t* btab;    // kBTables x kBEntries x kBStride
+  const int32_t* btab;    // kBTables x kBEntries x kBStride (the prep kernel's R side)
   // prep sides this launch runs: workgroup b runs side side0 + b % nsides
   // (0 hash, 1 A, 2 R); 0 / 3 = all three, 0 / 1 = the hash side, 1 / 2 = the points
   int32_t side0;
@@ -79,9 +79,9 @@ struct GlobalATab {
     for (int q = 0; q < 10; q++) p[q] = make_int4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
   }
 };
-// Shared 0..2^15 x B and 0..2^15 x 2^126 B tables in global memory (2 x 4 MiB,
-// L2/MALL-resident), read as 16-byte vectors: too large for LDS, and each lane
-// touches one 128-byte entry of each every fourth window.
+// The shared tables t = 0..11 of 0..2^21 x 2^(22 t) B in global memory (12 x 256
+// MiB), read as 16-byte vectors by the prep kernel's R side: one 128-byte entry
+// of each per signature.
 struct GlobalBTab {
   const int32_t* w;
   __device__ __forceinline__ ge_precomp entry(int tb, int j) const {

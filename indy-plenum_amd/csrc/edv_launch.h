@@ -15,7 +15,10 @@ hipError_t launch_main_kernel(unsigned blocks, hipStream_t s, const VerifyArgs& 
 // scatter with cursors ctr[kBuckets, 2 kBuckets) into perm (ctr zeroed by the caller)
 hipError_t launch_bucket_kernels(unsigned blocks, hipStream_t s, const uint64_t* off, uint64_t base, uint64_t n,
                                  uint32_t* ctr, uint32_t* perm);
-// the two shared B tables (kBTables x kBEntries x kBStride words), once per device
+// the shared [S]B tables, once per device: kBTabWords words at out, then the
+// tables' base points 2^(kBBits t) B (kBTables ge_p3) as scratch
+constexpr size_t kBTabWords = size_t(kBTables) * kBEntries * kBStride;
+constexpr size_t kBTabAllocBytes = 4 * kBTabWords + kBTables * sizeof(ge_p3);
 hipError_t launch_btab_kernel(hipStream_t s, int32_t* out);
 // the batch signer's comb rows (kCombRows x kCombEntries x kBStride words)
 hipError_t launch_comb_kernel(hipStream_t s, int32_t* out);

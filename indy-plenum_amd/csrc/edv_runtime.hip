@@ -244,7 +244,7 @@ int ctx_init(DevCtx& c) {
     if (v >= kBlock && v <= (uint64_t(1) << 24)) c.chunk = (v / kBlock) * kBlock;
   }
   if (c.st.ensure(c.chunk)) return EDV_E_OOM;
-  if (!c.btab) HIPOK(hipMalloc(&c.btab, kBTables * kBEntries * kBStride * 4), "hipMalloc btab");
+  if (!c.btab) HIPOK(hipMalloc(&c.btab, kBTabAllocBytes), "hipMalloc btab");
   if (!c.btab_built) {
     HIPOK(launch_btab_kernel(c.stream, c.btab), "btab launch");
     HIPOK(hipStreamSynchronize(c.stream), "btab sync");

@@ -7,14 +7,15 @@
 //   edv_prep_kernel (edv_prep.hip), three sides side by side:
 //     hash side  V2-V4 byte predicates, V6/V7 h = SHA-512(R || A || M) mod L
 //                straight from the caller's message buffer, the half-size
-//                scalars (a, b) with a = b h (mod 8L), b odd, and b S mod L,
-//                recoded into fixed signed windows
-//     A / R side decompress -A / -R (one sqrt exponentiation each) and build
-//                the per-signature 0..8 x P tables (cached form, HBM scratch)
-//   edv_main_kernel (below): [b S]B + [a](-A) + [b](-R) == identity by one
+//                scalars (a, b) with a = b h (mod 8L), b odd, recoded into
+//                fixed signed windows
+//     A side     decompress -A (one sqrt exponentiation), 0..8 x (-A) table
+//     R side     decompress -R, Q = [S]B - R (12 mixed additions against
+//                shared 0..2^21 x 2^(22 t) B tables), 0..8 x Q table
+//                (per-signature tables in cached form, HBM scratch)
+//   edv_main_kernel (below): [a](-A) + [b]([S]B - R) == identity by one
 //     joint walk of ~33 four-bit windows (FIXED windows, so all 64 lanes of a
-//     wave stay in lock-step), table entries staged through LDS, B digits
-//     every fourth window against two shared 0..2^15 tables; no inversion.
+//     wave stay in lock-step), table entries staged through LDS; no inversion.
 //   DESIGN.md section 2 has the argument that this is libsodium's verdict.
 // No MFMA: this is scalar bignum integer work (v_mad_i64_i32 chains).
 #include <hip/hip_runtime.h>
@@ -35,11 +36,9 @@ namespace {
 // (global_load_lds_dwordx4: 64 lanes x 16 B per instruction, lane-linear), so
 // nothing of it sits in registers during the window's doublings; fetch()
 // waits for the copies and reads the lane's 16-byte pieces back.  Per wave:
-// A 10 KiB + R 10 KiB = 20 KiB (80 KiB per 256-thread workgroup); the B
-// entries go to registers (RegBTab), so two 256-thread workgroups fit a CU (2
-// waves/SIMD once a chunk has more than one wave per SIMD: main 5.5 % faster at
-// 2^18 signatures than with the B entries staged through LDS as well, the same
-// at 2^16, profiles/r03/ab_main_s8.jsonl).
+// A 10 KiB + R 10 KiB = 20 KiB (80 KiB per 256-thread workgroup), so two
+// 256-thread workgroups fit a CU (2 waves/SIMD once a chunk has more than one
+// wave per SIMD).
 constexpr int kEntryPieces = 10;  // one cached entry: 10 pieces of 64 lanes x 4 words
 constexpr int kLdsAWords = kEntryPieces * 256;
 constexpr int kLdsWaveWords = 2 * kLdsAWords;
@@ -70,33 +69,6 @@ struct LdsATab {
     return c;
   }
 };
-// B entries straight into registers, loaded late in the window (issue() runs
-// after the R entry's LDS pick, so the loads fly during the R addition): no
-// LDS, at the price of 64 registers live across one addition every fourth
-// window.
-struct RegBTab {
-  const int32_t* w;
-  int j[kBTables];
-  int4 v[kBTables][8];
-  __device__ __forceinline__ void stage(int tb, int e) { j[tb] = e; }
-  __device__ __forceinline__ void issue() {
-#pragma unroll
-    for (int tb = 0; tb < kBTables; tb++) {
-      const int4* g = reinterpret_cast<const int4*>(w + (tb * kBEntries + j[tb]) * kBStride);
-#pragma unroll
-      for (int q = 0; q < 8; q++) v[tb][q] = g[q];
-    }
-  }
-  __device__ __forceinline__ ge_precomp fetch(int tb) {
-    int32_t t[32];
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      t[4 * q] = v[tb][q].x; t[4 * q + 1] = v[tb][q].y; t[4 * q + 2] = v[tb][q].z; t[4 * q + 3] = v[tb][q].w;
-    }
-    return precomp_from_words(t);
-  }
-};
-
 // Phase 2: V8 multi-scalar walk and the identity check.  The window count is
 // the wave's maximum over its live lanes, so the loop stays wave-uniform.
 // The main kernel's body, shared by edv_main_kernel and the split pipeline's
@@ -107,7 +79,7 @@ struct RegBTab {
 // the window loop: the digit registers are shifted inside the loop, and the
 // waitcnt pass, merging the loop's back edge with loads still pending from the
 // preheader, otherwise inserts vmcnt waits at the loop head and right after
-// the B-table loads, so every fourth window stalled on its table reads.)
+// the table stages.)
 #define EDV_MAIN_BODY \
   const uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x; \
   const bool live = j < a.n && a.st.alive[j] && a.st.alive[a.st.cap + j] && a.st.alive[2 * a.st.cap + j]; \
@@ -120,26 +92,21 @@ _Pragma("unroll") \
   nwin = __builtin_amdgcn_readfirstlane(nwin); \
   if (!live) return; \
   const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j); \
-  uint32_t da[8], db[8], bw[kBDigits]; \
+  uint32_t da[8], db[8]; \
 _Pragma("unroll") \
   for (int k = 0; k < 8; k++) { \
     da[k] = d[uint64_t(k) * cap]; \
     db[k] = d[uint64_t(8 + k) * cap]; \
   } \
 _Pragma("unroll") \
-  for (int k = 0; k < kBDigits; k++) bw[k] = d[uint64_t(kDigB + k) * cap]; \
-_Pragma("unroll") \
   for (int k = 0; k < 8; k++) { \
     da[k] = uint32_t(opaque_i32(int32_t(da[k]))); \
     db[k] = uint32_t(opaque_i32(int32_t(db[k]))); \
   } \
-_Pragma("unroll") \
-  for (int k = 0; k < kBDigits; k++) bw[k] = uint32_t(opaque_i32(int32_t(bw[k]))); \
   int32_t* wl = lds_main + (threadIdx.x >> 6) * kLdsWaveWords; \
   const int lane = int(threadIdx.x & 63); \
   LdsATab at{a.st.atab + j * kAWords, wl, lane}, rt{a.st.rtab + j * kAWords, wl + kLdsAWords, lane}; \
-  RegBTab bt{a.btab, {0, 0}, {}}; \
-  a.accept[i] = main_one(da, db, bw, nwin, (wf >> 8) & 1, at, rt, bt) ? 1 : 0;
+  a.accept[i] = main_one(da, db, nwin, (wf >> 8) & 1, at, rt) ? 1 : 0;
 
 __global__ __launch_bounds__(kBlock) void edv_main_kernel(VerifyArgs a) {
   __shared__ int32_t lds_main[(kBlock / 64) * kLdsWaveWords];
@@ -282,10 +249,15 @@ __global__ __launch_bounds__(kBlock) void edv_flush_kernel(int4* p, uint64_t n16
   }
 }
 
-// j * B and j * 2^kBSplit B for j = 0..2^(kBBits-1) in affine precomp form, once per device
-__global__ void edv_btab_kernel(int32_t* out) {
-  const int t = threadIdx.x + blockIdx.x * blockDim.x;
-  if (t < kBTables * kBEntries) btab_entry(out + t * kBStride, t % kBEntries, base_point((t / kBEntries) * kBSplit));
+// The [S]B tables, once per device: the base points 2^(kBBits t) B first
+// (one lane each), then j x base t for t = 0..kBTables-1, j = 0..2^(kBBits-1),
+// affine precomp form, one entry per lane.
+__global__ void edv_bbase_kernel(ge_p3* bases) {
+  if (threadIdx.x < kBTables) bases[threadIdx.x] = base_point(int(threadIdx.x) * kBBits);
+}
+__global__ void edv_btab_kernel(int32_t* out, const ge_p3* bases) {
+  const uint32_t t = threadIdx.x + blockIdx.x * blockDim.x;
+  if (t < uint32_t(kBTables * kBEntries)) btab_entry(out + size_t(t) * kBStride, int(t % kBEntries), bases[t / kBEntries]);
 }
 
 // Row f-3: SHA-256 of n messages, one per lane -> 32-byte digests (out: n x 8 words).
@@ -318,7 +290,9 @@ hipError_t launch_bucket_kernels(unsigned blocks, hipStream_t s, const uint64_t*
   return hipGetLastError();
 }
 hipError_t launch_btab_kernel(hipStream_t s, int32_t* out) {
-  edv_btab_kernel<<<(kBTables * kBEntries + 63) / 64, 64, 0, s>>>(out);
+  ge_p3* bases = reinterpret_cast<ge_p3*>(out + kBTabWords);
+  edv_bbase_kernel<<<1, 64, 0, s>>>(bases);
+  edv_btab_kernel<<<(kBTables * kBEntries + 63) / 64, 64, 0, s>>>(out, bases);
   return hipGetLastError();
 }
 hipError_t launch_comb_kernel(hipStream_t s, int32_t* out) {

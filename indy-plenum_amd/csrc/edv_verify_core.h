@@ -15,37 +15,39 @@ namespace edv {
 // with a 253-bit h costs 252 doublings.  Instead the prep kernel finds, by a
 // 2-dimensional lattice reduction, a ~128-bit pair (a, b) with a = b h (mod 8L)
 // and b odd, and the main kernel checks
-//     [b S mod L]B + [a](-A) + [b](-R) == identity
-// which is [b](R' - R) == 0: since b is odd and 0 < |b| < L, that holds iff
+//     [a](-A) + [b]([S]B - R) == identity
+// which is [b](R' - R) == 0 ([b]([S]B) = [b S mod L]B: B has order L): since b is odd and 0 < |b| < L, that holds iff
 // R' == R (the group has order 8L; a = b h mod 8L, not just mod L, keeps the
 // torsion part of a mixed-order A exact).  R' == R is libsodium's
 // encode(R') == R bytes for canonical, decodable R; any other R is rejected
 // up front, as libsodium's compare would.  ~130 doublings instead of 252, and
 // no inversion at the end; the price is a second decompression (R) and a
-// second per-lane table in the prep kernel.
+// second per-lane table in the prep kernel.  [S]B needs only the signature,
+// not h: the prep kernel's R side computes it (12 mixed additions against
+// shared tables) and builds the second table on [S]B - R, so the main kernel's
+// walk has no fixed-base part and the h-dependent critical path of a
+// synchronous call (copy -> hash side -> main) carries none of that work.
 //
-// [a](-A), [b](-R): fixed signed windows of kAWin bits against per-lane tables
-// 0..2^(kAWin-1) x (-A) and x (-R); the window count is the wave's maximum
-// over its lanes.  Default kAWin = 4: digits in [-8, 7] (the top one >= 0),
+// [a](-A), [b](S B - R): fixed signed windows of kAWin bits against per-lane
+// tables 0..2^(kAWin-1) x (-A) and x (S B - R); the window count is the wave's
+// maximum over its lanes.  Default kAWin = 4: digits in [-8, 7] (the top one >= 0),
 // 9-entry tables, 33 windows in practice (34 for a few waves), at most 64.
-// [b S mod L]B = [s_lo]B + [s_hi](2^126 B): 8 signed radix-2^16 digits of each
-// half against shared tables 0..2^15 x B and 0..2^15 x 2^126 B (4 MiB each),
-// both added at every fourth window (16 = 4 x 4 bits) from window 28 down.
 // (5-bit windows -- 17-entry tables, ~27 windows -- made the prep kernel 17 %
 // slower for a main kernel 3 % faster, net -5 %: profiles/r02/ab_w4_s43.jsonl.)
-constexpr int kAWin = 4;                        // bits per [a](-A) / [b](-R) window
+constexpr int kAWin = 4;                        // bits per [a](-A) / [b](SB - R) window
 constexpr int kAWindows = (255 + kAWin - 1) / kAWin;  // at most: 64 x 4 = 256 bits >= 253
 constexpr int kAEntries = (1 << (kAWin - 1)) + 1;     // per-lane table 0..8 x P, cached form (entry 0 = identity)
-constexpr int kBBits = 16;                      // radix 2^16 digits of the B scalar halves
-constexpr int kBSplit = 126;                    // s = s_lo + 2^126 s_hi
-// digits per half: 8 x 16 = 128 bits for s_lo < 2^126 and s_hi < 2^127; s_hi's top
-// digit may reach 2^15, which 16-bit two's complement cannot hold: main_one reads that one digit unsigned
-constexpr int kBDigits = 8;
-constexpr int kBEvery = kBBits / kAWin;         // a B digit every fourth window
-constexpr int kBMinWindows = kBEvery * (kBDigits - 1) + 1;  // 29: the walk reaches window 28
-constexpr int kBEntries = (1 << (kBBits - 1)) + 1; // per table 0..2^15 x base, affine precomp form, 4 MiB
-constexpr int kBTables = 2;                     // base B and base 2^kBSplit B
-static_assert(kBBits % kAWin == 0, "B digits must land on window boundaries");
+// [S]B (prep kernel, R side): 12 signed radix-2^22 digits of S against shared
+// tables t = 0..11 of 0..2^21 x 2^(22 t) B (affine precomp form, 256 MiB each,
+// 3 GiB per device: memory the 288 GB of HBM has to spare buys mixed additions --
+// radix 2^16 (16 additions, 64 MiB) made the C2 step 1.1 % slower, 2^19 (14)
+// 0.8 %, profiles/r05/ab_bbits_s13.jsonl; the gathers are staged ahead, so the
+// tables' size costs no latency)
+constexpr int kBBits = 22;
+constexpr int kBTables = (253 + kBBits - 1) / kBBits;  // 12: digit t of S against table t
+constexpr int kBEntries = (1 << (kBBits - 1)) + 1;     // per table 0..2^(kBBits-1) x base
+// the top digit, (S >> kBBits (kBTables - 1)) + carry, must index its table too
+static_assert(253 - kBBits * (kBTables - 1) <= kBBits - 1, "top [S]B digit out of table range");
 constexpr int kCombEntries = 129;               // signer comb rows: 0..128 x 256^i B
 constexpr int kBStride = 32;                    // words per B / comb entry (30 used; 128-byte aligned)
 
@@ -205,9 +207,6 @@ EDV_HD void recode8(uint32_t out[8], const uint32_t s[8]) {
     out[w] = packed;
   }
 }
-// 17 signed radix-2^15 digits of a scalar < 2^253 (kept for the recoding tests)
-EDV_HD void recode15(uint32_t out[8], const uint32_t s[8]) { recode_signed<15, 17>(out, s); }
-EDV_HD void recode16(uint32_t out[8], const uint32_t s[8]) { recode_signed<16, 16>(out, s); }
 
 // Number of windows the packed radix-2^kAWin digits need: 1 + index of the
 // top nonzero digit (0 for a zero scalar).
@@ -531,62 +530,19 @@ EDV_HD void half_scalars(const uint32_t h[8], uint32_t a[8], uint32_t u[8], bool
   }
 }
 
-// (u * S) mod L for u < 2^256, S < 2^256 (8 words each).  Row by row: each
-// step u_i s_j + t_(i+j) + carry < 2^64 exactly, so it is one 32x32+64
-// multiply-add and one 64-bit add with no carry detection (the column form
-// needed a 64-bit compare and a select per product: 925 instructions, now ~200).
-EDV_HD void sc_mul(uint32_t out[8], const uint32_t u[8], const uint32_t s[8]) {
-  uint32_t t[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) t[k] = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint64_t carry = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const uint64_t p = uint64_t(u[i]) * s[j] + t[i + j] + carry;
-      t[i + j] = uint32_t(p);
-      carry = p >> 32;
-    }
-    t[i + 8] = uint32_t(carry);
-  }
-  sc_reduce(out, t);
-}
-
-// B-scalar digits of s < L: word k (k < kBDigits) = radix-2^kBBits digit k of
-// s_lo = s mod 2^kBSplit in its low 16 bits and digit k of s_hi = s >> kBSplit
-// in its high 16 bits, signed (two's complement in 16 bits, |d| <= 2^(kBBits-1),
-// top digits >= 0; s_hi's top digit is read unsigned, see kBDigits).
-EDV_HD void recode_bscalar(uint32_t bw[kBDigits], const uint32_t s[8]) {
-  uint32_t lo[8], hi[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const int src = i + kBSplit / 32;
-    const uint32_t w0 = src < 8 ? s[src] : 0, w1 = src + 1 < 8 ? s[src + 1] : 0;
-    hi[i] = (w0 >> (kBSplit % 32)) | (w1 << (32 - kBSplit % 32));
-    lo[i] = i < kBSplit / 32 ? s[i] : (i == kBSplit / 32 ? s[i] & ((1u << (kBSplit % 32)) - 1) : 0);
-  }
-  uint32_t dl[8], dh[8];
-  recode_signed<kBBits, kBDigits>(dl, lo);
-  recode_signed<kBBits, kBDigits>(dh, hi);
-#pragma unroll
-  for (int k = 0; k < kBDigits; k++) {
-    const int pos = kBBits * k, wi = pos >> 5, sh = pos & 31;
-    const uint64_t wl = uint64_t(dl[wi]) | (wi + 1 < 8 ? uint64_t(dl[wi + 1]) << 32 : 0);
-    const uint64_t wh = uint64_t(dh[wi]) | (wi + 1 < 8 ? uint64_t(dh[wi + 1]) << 32 : 0);
-    // sign-extend the kBBits-bit fields to 16 bits (radix 2^16: already 16 bits)
-    constexpr int kX = 32 - kBBits;
-    const uint32_t el = uint32_t(int32_t(uint32_t(wl >> sh) << kX) >> kX) & 0xffffu;
-    const uint32_t eh = uint32_t(int32_t(uint32_t(wh >> sh) << kX) >> kX) & 0xffffu;
-    bw[k] = el | (eh << 16);
-  }
-}
 // shift a 256-bit little-endian word vector left by N bits (0 < N < 32)
 template <int N>
 EDV_HD void shl256(uint32_t v[8]) {
 #pragma unroll
   for (int i = 7; i > 0; i--) v[i] = (v[i] << N) | (v[i - 1] >> (32 - N));
   v[0] <<= N;
+}
+// ... and right by N bits (0 < N < 32)
+template <int N>
+EDV_HD void shr256(uint32_t v[8]) {
+#pragma unroll
+  for (int i = 0; i < 7; i++) v[i] = (v[i] >> N) | (v[i + 1] << (32 - N));
+  v[7] >>= N;
 }
 
 EDV_HD ge_precomp precomp_from_words(const int32_t* w) {
@@ -626,10 +582,9 @@ EDV_HD void btab_entry(int32_t* o, int j, const ge_p3& base) {
 // Per-lane outputs of phase 1 that phase 2 consumes.
 struct PrepDigits {
   uint32_t da[8];        // packed signed radix-2^kAWin digits of a ([a](-A))
-  uint32_t db[8];        // packed signed radix-2^kAWin digits of |b| ([b](-R), sign folded into the R table)
-  uint32_t bw[kBDigits]; // B-scalar digit pairs (recode_bscalar)
+  uint32_t db[8];        // packed signed radix-2^kAWin digits of |b| ([b](SB - R), sign folded into the walk)
   int nwin;              // windows this lane needs (max over a and |b|)
-  bool negR;             // b < 0: the R digits are negated ([b](-R) = [|b|](R))
+  bool negR;             // b < 0: the second table's digits are negated ([b]Q = [|b|](-Q))
 };
 
 // 0..kAEntries-1 x P into a per-lane table (entry 0 the identity, so a zero digit needs
@@ -650,39 +605,43 @@ EDV_HD void build_table(Tab& tab, const ge_p3& P) {
     tab.store(e, ge_p3_to_cached(cur));
   }
 }
+// The same for a projective P (Z != 1): full additions of P's cached form,
+// which Stash keeps outside the registers between them (put(c), get(); on the
+// GPU the lane's LDS slice) -- held live across the loop, its 40 registers
+// made the prep kernel spill inside it (prep +9 % at C2).
+template <class Tab, class Stash>
+EDV_HD void build_table_projective(Tab& tab, const ge_p3& P, Stash& st) {
+  {
+    const ge_cached c1 = ge_p3_to_cached(P);
+    tab.store(0, ge_cached_identity());
+    tab.store(1, c1);
+    st.put(c1);
+  }
+  ge_p3 cur = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(P)));
+  tab.store(2, ge_p3_to_cached(cur));
+#pragma unroll 1
+  for (int e = 3; e < kAEntries; e++) {
+    cur = ge_p1p1_to_p3(ge_add(cur, st.get()));
+    tab.store(e, ge_p3_to_cached(cur));
+  }
+}
 
 // Phase 1, hash side (kernel edv_prep_kernel): strictness checks V2-V4,
-// h = SHA-512(R || A || M) mod L (V6, V7), the half-size scalars (a, b), the B
-// scalar b S mod L and the digit recoding.  Returns false if the signature is
-// already rejected (then the digits are unspecified).
+// h = SHA-512(R || A || M) mod L (V6, V7), the half-size scalars (a, b) and
+// their digit recoding.  Returns false if the signature is already rejected
+// (then the digits are unspecified).
 EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[8], const uint8_t* m, uint64_t mlen,
                      PrepDigits& pd) {
   bool ok = !((S[7] & 0xF0000000u) && !sc_is_canonical(S));
   ok = ok && !has_small_order(R);
   ok = ok && ge_is_canonical(A) && !has_small_order(A);
   if (!ok) return false;
-  // hash and lattice first, points after: the two decompressions and tables
-  // then run one after the other with little else live (register pressure)
   uint32_t dig[16], h[8];
   hram(dig, R, A, m, mlen);
   sc_reduce(h, dig);
   uint32_t a[8], u[8];
   bool neg;
   half_scalars(h, a, u, neg);
-  // B scalar: b S mod L with b = (neg ? -u : u)
-  uint32_t s[8];
-  sc_mul(s, u, S);
-  const uint32_t L[8] = {0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu, 0, 0, 0, 0x10000000u};
-  const bool sz = (s[0] | s[1] | s[2] | s[3] | s[4] | s[5] | s[6] | s[7]) == 0;
-  if (neg && !sz) {
-    uint32_t t[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) t[i] = L[i];
-    w8_sub(t, s);
-#pragma unroll
-    for (int i = 0; i < 8; i++) s[i] = t[i];
-  }
-  recode_bscalar(pd.bw, s);
   recode5(pd.da, a);
   recode5(pd.db, u);
   pd.nwin = mx(digits5_windows(pd.da), digits5_windows(pd.db));
@@ -690,12 +649,9 @@ EDV_HD bool prep_one(const uint32_t R[8], const uint32_t S[8], const uint32_t A[
   return true;
 }
 
-// Phase 1, point sides (kernel edv_prep_kernel, concurrent with the hash
-// side): decompress -P and build its 0..kAEntries-1 x (-P) table, for P = A (V4, V5:
-// libsodium's checks on the key) and for P = R.  encode(R') is canonical and a
-// curve point's encoding, so R bytes that are non-canonical, of small order
-// (libsodium's blocklist) or decode to no point can never pass: the same three
-// checks reject them.  Returns false on rejection.
+// Phase 1, A side (kernel edv_prep_kernel, concurrent with the hash side):
+// decompress -A and build its 0..kAEntries-1 x (-A) table (V4, V5: libsodium's
+// checks on the key).  Returns false on rejection.
 template <class ATab>
 EDV_HD bool prep_point(const uint32_t P[8], ATab& tab) {
   if (!ge_is_canonical(P) || has_small_order(P)) return false;
@@ -705,18 +661,59 @@ EDV_HD bool prep_point(const uint32_t P[8], ATab& tab) {
   return true;
 }
 
-// Phase 2 (kernel edv_main_kernel): Q = [s_lo]B + [s_hi](2^kBSplit B) + [a](-A) +
-// [|b|](-+R) by a joint fixed-window walk, top window first -- every lane adds
-// at the same positions, so a wave never diverges -- then Q == identity.
-// nwin: windows to walk (the wave's maximum; >= every lane's own count);
-// da/db are consumed from the top (shifted left 5 bits per window), bw from
-// entry kBDigits-1 down.  ATab provides stage(e) then fetch() -> cached entry e;
-// BTab stage(t, j), issue() (after the R entry's pick: the register
-// variant starts its loads there) then fetch(t) -> entry j of table t.
+// Phase 1, R side: Q = [S]B - R and its 0..kAEntries-1 x Q table.  encode(R')
+// is canonical and a curve point's encoding, so R bytes that are
+// non-canonical, of small order (libsodium's blocklist) or decode to no point
+// can never pass: the same three checks as for A reject them.  [S]B is the
+// sum of entry |d_t| of table t (negated for d_t < 0) over the kBTables signed
+// radix-2^kBBits digits d_t of S, added to -R by mixed additions; BTab provides
+// stage(t, j) then fetch() -> j x 2^(kBBits t) B (precomp).  S < L for every signature that can
+// pass (the hash side's V2 check rejects the rest); S is cut to 253 bits so
+// that any 256-bit S keeps its digits inside the tables.  BTab also stashes
+// Q's cached form for the table (build_table_projective).
 template <class ATab, class BTab>
-EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int nwin, bool negR, ATab& at, ATab& rt,
-                     BTab& bt) {
-  nwin = mx(nwin, kBMinWindows);
+EDV_HD bool prep_rpoint(const uint32_t R[8], const uint32_t S[8], ATab& tab, BTab& bt) {
+  if (!ge_is_canonical(R) || has_small_order(R)) return false;
+  ge_p3 q;
+  if (!ge_frombytes_negate(q, R)) return false;
+  uint32_t s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = S[i];
+  s[7] &= 0x1fffffffu;
+  // signed digits, least significant first, taken off the bottom of s as the
+  // walk goes: d = (s mod 2^kBBits) + carry in [-2^(kBBits-1), 2^(kBBits-1));
+  // the top digit keeps its carry (static_assert above: it stays in range)
+  int carry = 0;
+  auto next_digit = [&](bool top) {
+    int e = int(s[0] & ((1u << kBBits) - 1)) + carry;
+    shr256<kBBits>(s);
+    carry = top ? 0 : (e + (1 << (kBBits - 1))) >> kBBits;
+    return e - carry * (1 << kBBits);
+  };
+  // entry t + 1 is staged (on the GPU: straight into LDS) while entry t is added
+  int dt = next_digit(kBTables == 1);
+  bt.stage(0, dt < 0 ? -dt : dt);
+#pragma unroll 1
+  for (int t = 0; t < kBTables; t++) {
+    const ge_precomp e = ge_precomp_cneg(bt.fetch(), dt < 0);
+    if (t + 1 < kBTables) {
+      dt = next_digit(t + 2 == kBTables);
+      bt.stage(t + 1, dt < 0 ? -dt : dt);
+    }
+    q = ge_p1p1_to_p3(ge_madd(q, e));
+  }
+  build_table_projective(tab, q, bt);
+  return true;
+}
+
+// Phase 2 (kernel edv_main_kernel): Q = [a](-A) + [|b|](+-([S]B - R)) by a
+// joint fixed-window walk, top window first -- every lane adds at the same
+// positions, so a wave never diverges -- then Q == identity.  nwin: windows to
+// walk (the wave's maximum; >= every lane's own count); da/db are consumed
+// from the top (shifted left kAWin bits per window).  ATab provides stage(e)
+// then fetch() -> cached entry e.
+template <class ATab>
+EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], int nwin, bool negR, ATab& at, ATab& rt) {
   // align window nwin-1 with the top window, bits [kTop, kTop + kAWin)
   constexpr int kTop = kAWin * (kAWindows - 1);       // 250 (252)
   constexpr int kTopShl = 32 - kAWin - (kTop - 224);  // 1 (0)
@@ -736,18 +733,6 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
     shl256<kAWin>(db);
     at.stage(dA < 0 ? -dA : dA);
     rt.stage(dR < 0 ? -dR : dR);
-    const bool addB = (w % kBEvery) == 0 && w < kBMinWindows;
-    int d0 = 0, d1 = 0;
-    if (addB) {
-      const uint32_t pair = bw[kBDigits - 1];
-#pragma unroll
-      for (int k = kBDigits - 1; k > 0; k--) bw[k] = bw[k - 1];
-      d0 = int32_t(pair << 16) >> 16;
-      // radix 2^16: s_hi's top digit (the first one walked) may be 2^15, kept unsigned
-      d1 = (kBBits == 16 && w == kBMinWindows - 1) ? int32_t(pair >> 16) : int32_t(pair) >> 16;
-      bt.stage(0, d0 < 0 ? -d0 : d0);
-      bt.stage(1, d1 < 0 ? -d1 : d1);
-    }
     ge_p3 p3;
     if (w == nwin - 1) {
       p3 = ge_p3_identity();
@@ -759,14 +744,7 @@ EDV_HD bool main_one(uint32_t da[8], uint32_t db[8], uint32_t bw[kBDigits], int 
     const ge_cached ea = at.fetch();
     p3 = ge_p1p1_to_p3(ge_add(p3, ge_cached_cneg(ea, dA < 0)));
     const ge_cached er = rt.fetch();
-    if (addB) bt.issue();
-    ge_p1p1 t = ge_add(p3, ge_cached_cneg(er, (dR < 0) != negR));
-    if (addB) {
-      p3 = ge_p1p1_to_p3(t);
-      p3 = ge_p1p1_to_p3(ge_madd(p3, ge_precomp_cneg(bt.fetch(0), d0 < 0)));
-      t = ge_madd(p3, ge_precomp_cneg(bt.fetch(1), d1 < 0));
-    }
-    acc = ge_p1p1_to_p2(t);
+    acc = ge_p1p1_to_p2(ge_add(p3, ge_cached_cneg(er, (dR < 0) != negR)));
   }
   // identity: X = 0 and Y = Z (mod p)
   return fe_iszero(acc.X) && fe_iszero(fe_carry32(fe_sub(acc.Y, acc.Z)));
@@ -779,8 +757,8 @@ EDV_HD bool verify_one(const uint32_t R[8], const uint32_t S[8], const uint32_t 
                        ATab& at, ATab& rt, BTab& bt) {
   PrepDigits pd;
   if (!prep_one(R, S, A, m, mlen, pd)) return false;
-  if (!prep_point(A, at) || !prep_point(R, rt)) return false;
-  return main_one(pd.da, pd.db, pd.bw, pd.nwin, pd.negR, at, rt, bt);
+  if (!prep_point(A, at) || !prep_rpoint(R, S, rt, bt)) return false;
+  return main_one(pd.da, pd.db, pd.nwin, pd.negR, at, rt);
 }
 
 // ------------------------------------------------ batch signing (row f-4)

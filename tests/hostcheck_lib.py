@@ -21,10 +21,9 @@ def load():
         _lib.hc_hram.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
         _lib.hc_sha256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
         _lib.hc_recode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p]
-        _lib.hc_btab.argtypes = [ctypes.c_void_p]
-        _lib.hc_btab_table.argtypes = [ctypes.c_int, ctypes.c_void_p]
+        _lib.hc_btab_entries_of.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        _lib.hc_rside_point.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p]
         _lib.hc_half_scalars.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p]
-        _lib.hc_recode_bscalar.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
         _lib.hc_verify_batch.argtypes = [ctypes.c_char_p] * 3 + [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
         _lib.hc_layout.argtypes = [ctypes.c_void_p]
         _lib.hc_ledger.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
@@ -34,9 +33,9 @@ def load():
 
 def layout():
     """The walk's layout constants as built (edv_verify_core.h)."""
-    out = (ctypes.c_int32 * 7)()
+    out = (ctypes.c_int32 * 4)()
     load().hc_layout(out)
-    return dict(zip(("awin", "aentries", "bbits", "bsplit", "bdigits", "bevery", "bminwindows"), list(out)))
+    return dict(zip(("awin", "aentries", "bbits", "btables"), list(out)))
 
 
 def ledger(n, failed, queries):

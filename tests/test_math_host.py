@@ -206,11 +206,10 @@ def _digits(packed, bits):
     return out
 
 
-def test_scalar_recoding_radix_4_5_8_15_16():
+def test_scalar_recoding_radix_4_5_8():
     """Signed digits: radix 16 (the main loop's windows, digit in [-8, 7], so |d|
-    indexes the 0..8 per-lane table) and radix 32 (the EDV_AWIN=5 layout),
-    signer scalars (radix 256), the generic recoder at radix 2^15 / 2^16 (B
-    digits); sum d_k * 2^(bits*k) must give back the scalar."""
+    indexes the 0..8 per-lane table) and radix 32, signer scalars (radix 256);
+    sum d_k * 2^(bits*k) must give back the scalar."""
     hc = hostcheck_lib.load()
     r = random.Random(12)
     out = (ctypes.c_uint32 * 8)()
@@ -219,7 +218,7 @@ def test_scalar_recoding_radix_4_5_8_15_16():
     edge += [int("8000" * 16, 16) % L, int("7fff" * 16, 16) % L, int("ffff" * 15, 16), int("80" * 31, 16)]
     edge += [int("88" * 31, 16), int("77" * 31, 16)]
     vals = [v for v in edge if 0 <= v < L] + [r.randrange(L) for _ in range(2000)]
-    for bits, lo, hi in ((4, -8, 7), (5, -16, 15), (8, -128, 127), (15, -2**14, 2**14), (16, -2**15, 2**15)):
+    for bits, lo, hi in ((4, -8, 7), (5, -16, 15), (8, -128, 127)):
         for v in vals:
             assert hc.hc_recode(v.to_bytes(32, "little"), bits, out) == 0
             d = _digits(list(out), bits)
@@ -229,52 +228,117 @@ def test_scalar_recoding_radix_4_5_8_15_16():
 
 
 def test_walk_layout_constants():
-    """The default build walks 4-bit windows (9-entry per-lane tables) with
-    radix-2^16 B digits split at 2^126, added every fourth window from window 28."""
+    """The default build walks 4-bit windows (9-entry per-lane tables); the R
+    side computes [S]B from 12 signed radix-2^22 digits against 12 tables."""
     lay = hostcheck_lib.layout()
-    assert lay == {"awin": 4, "aentries": 9, "bbits": 16, "bsplit": 126, "bdigits": 8, "bevery": 4,
-                   "bminwindows": 29}
-    # both halves of any B scalar s < L fit their digits: s_lo < 2^126, s_hi < 2^127
-    assert lay["bdigits"] * lay["bbits"] >= max(lay["bsplit"], L.bit_length() - lay["bsplit"]) + 1
+    assert lay == {"awin": 4, "aentries": 9, "bbits": 22, "btables": 12}
+    # every S < 2^253 fits the digits, the top one (carry included) its table
+    assert lay["bbits"] * lay["btables"] >= 253 and 253 - lay["bbits"] * (lay["btables"] - 1) <= lay["bbits"] - 1
 
 
-def test_btab_entries_are_multiples_of_B():
-    """The 0..2^(bbits-1) x B table (affine y+x, y-x, 2dxy limbs) against the oracle's [j]B."""
+def _btab_entries(hc, t, js):
+    import numpy as np
+    js = np.asarray(js, np.int32)
+    out = np.zeros(32 * len(js), np.int32)
+    assert hc.hc_btab_entries_of(t, js.ctypes.data, len(js), out.ctypes.data) == 0
+    return out.reshape(len(js), 32)
+
+
+def test_btab_entries_are_multiples_of_2_16t_B():
+    """Table t of the R side's [S]B: entry j = j x 2^(bbits t) B (affine y+x, y-x,
+    2dxy limbs) against the oracle's fixed-base multiplication, for the first,
+    a middle and the last table."""
     import oracle_lib as orc
     hc = hostcheck_lib.load()
-    lay = hostcheck_lib.layout()
     n = hc.hc_btab_entries()
-    assert n == 2**(lay["bbits"] - 1) + 1
-    tab = (ctypes.c_int32 * (n * 32))()
-    hc.hc_btab(tab)
+    assert n == 2**(hostcheck_lib.layout()["bbits"] - 1) + 1
     d = (-121665 * pow(121666, P - 2, P)) % P
+    inv2 = pow(2, P - 2, P)
     r = random.Random(13)
-    for j in [0, 1, 2, 3, 127, 128, 129, 255, 256, 4097, 16383, 16384, n - 2, n - 1] + [r.randrange(n) for _ in range(40)]:
-        e = list(tab[32 * j: 32 * j + 32])
-        ypx, ymx, xy2d = val(e[0:10]) % P, val(e[10:20]) % P, val(e[20:30]) % P
-        inv2 = pow(2, P - 2, P)
-        y, x = (ypx + ymx) * inv2 % P, (ypx - ymx) * inv2 % P
-        assert xy2d == 2 * d * x * y % P, j
-        enc = int.to_bytes(y | ((x & 1) << 255), 32, "little")
-        assert enc == orc.scalarmult_base(j.to_bytes(32, "little")), j
+    nt, bb = hostcheck_lib.layout()["btables"], hostcheck_lib.layout()["bbits"]
+    for t in (0, 1, nt // 2, nt - 1):
+        js = [0, 1, 2, 3, 127, 128, 255, 256, 4097, 16384, n - 2, n - 1] + [r.randrange(n) for _ in range(12)]
+        for j, e in zip(js, _btab_entries(hc, t, js)):
+            e = list(e)
+            ypx, ymx, xy2d = val(e[0:10]) % P, val(e[10:20]) % P, val(e[20:30]) % P
+            y, x = (ypx + ymx) * inv2 % P, (ypx - ymx) * inv2 % P
+            assert xy2d == 2 * d * x * y % P, (t, j)
+            enc = int.to_bytes(y | ((x & 1) << 255), 32, "little")
+            assert enc == orc.scalarmult_base(((j << (bb * t)) % L).to_bytes(32, "little")), (t, j)
 
 
-def test_btab_second_table_is_multiples_of_2_bsplit_B():
-    """Table 1 of the B-scalar walk: j x 2^bsplit B (s = s_lo + 2^bsplit s_hi),
-    against the oracle's [j 2^bsplit]B."""
+def _ed_add(p1, p2):
+    d = (-121665 * pow(121666, P - 2, P)) % P
+    (x1, y1), (x2, y2) = p1, p2
+    t = d * x1 * x2 * y1 * y2 % P
+    return ((x1 * y2 + y1 * x2) * pow(1 + t, P - 2, P) % P, (y1 * y2 + x1 * x2) * pow(1 - t, P - 2, P) % P)
+
+
+def _ed_decode(b):
+    d = (-121665 * pow(121666, P - 2, P)) % P
+    v = int.from_bytes(b, "little")
+    y, sign = v & ((1 << 255) - 1), v >> 255
+    if y >= P:
+        return None
+    u, w = (y * y - 1) % P, (d * y * y + 1) % P
+    x = pow(u * pow(w, P - 2, P), (P + 3) // 8, P)
+    if (w * x * x - u) % P:
+        x = x * pow(2, (P - 1) // 4, P) % P
+    if (w * x * x - u) % P:
+        return None
+    if x == 0 and sign:
+        return None
+    if (x & 1) != sign:
+        x = P - x
+    return x, y
+
+
+def _ed_encode(pt):
+    x, y = pt
+    return int.to_bytes(y | ((x & 1) << 255), 32, "little")
+
+
+def test_r_side_point_is_SB_minus_R():
+    """The prep kernel's R side: Q = [S]B - R from the signed radix-2^bbits digits of S,
+    against Python affine arithmetic on the oracle's [S]B, for S over the range
+    V2 admits (edges and random, below L and below 2^252) and R of every
+    order: a valid signature's R, torsion-shifted R, the identity-adjacent
+    cases; rejected R (small order, non-canonical, not on the curve) gives -1."""
     import oracle_lib as orc
     hc = hostcheck_lib.load()
-    split = hostcheck_lib.layout()["bsplit"]
-    n = hc.hc_btab_entries()
-    tab = (ctypes.c_int32 * (n * 32))()
-    assert hc.hc_btab_table(1, tab) == 0
-    inv2 = pow(2, P - 2, P)
-    for j in [0, 1, 2, 3, 255, 8191, 16384, n - 1]:
-        e = list(tab[32 * j: 32 * j + 32])
-        ypx, ymx = val(e[0:10]) % P, val(e[10:20]) % P
-        y, x = (ypx + ymx) * inv2 % P, (ypx - ymx) * inv2 % P
-        enc = int.to_bytes(y | ((x & 1) << 255), 32, "little")
-        assert enc == orc.scalarmult_base(((j << split) % L).to_bytes(32, "little")), j
+    r = random.Random(31)
+    out = ctypes.create_string_buffer(32)
+    bb = hostcheck_lib.layout()["bbits"]
+    # digit edges: |d| = 2^(bb-1) (the last entry) with and without carries, all-ones runs
+    Ss = [0, 1, 2, 2**bb - 1, 2**bb, 2**(bb - 1), 2**(bb - 1) - 1, 2**(bb - 1) + 1, L - 1, L - 2, 2**252 - 1]
+    Ss += [2**(bb * k) - 1 for k in range(2, 12) if 2**(bb * k) < L] + [2**(bb - 1) * (2**(bb * k) - 1) // (2**bb - 1) % L for k in (3, 11)]
+    Ss += [2**240, 2**252 - 2**240, sum(2**(bb * k + bb - 1) for k in range(11)) % L]
+    Ss += [int("8000" * 16, 16) % L, int("7fff" * 16, 16) % L] + [r.randrange(L) for _ in range(60)]
+    pts = []
+    for _ in range(8):
+        k = r.randrange(1, L)
+        pts.append(orc.scalarmult_base(k.to_bytes(32, "little")))
+    # a mixed-order R: a valid point plus the order-2 point (0, -1)
+    q = _ed_decode(pts[0])
+    pts.append(_ed_encode(_ed_add(q, (0, P - 1))))
+    for S in Ss:
+        sb = _ed_decode(orc.scalarmult_base(S.to_bytes(32, "little")))
+        for Rb in pts + ([orc.scalarmult_base(S.to_bytes(32, "little"))] if S else []):  # R = [S]B: Q = identity
+            Rp = _ed_decode(Rb)
+            want = _ed_encode(_ed_add(sb, ((P - Rp[0]) % P, Rp[1])))
+            assert hc.hc_rside_point(Rb, S.to_bytes(32, "little"), out) == 0, (hex(S), Rb.hex())
+            assert out.raw == want, (hex(S), Rb.hex())
+    # S with bits above 2^253 (rejected by the hash side): no fault, some point
+    for S in (2**256 - 1, 2**255 + 12345, 2**253):
+        assert hc.hc_rside_point(pts[1], S.to_bytes(32, "little"), out) == 0
+    # rejected R: identity (small order), y >= p (non-canonical), not on the curve
+    bad = [_ed_encode((0, 1)), (P + 1).to_bytes(32, "little")]
+    y = 2
+    while _ed_decode(y.to_bytes(32, "little")) is not None:
+        y += 1
+    bad.append(y.to_bytes(32, "little"))
+    for Rb in bad:
+        assert hc.hc_rside_point(Rb, (5).to_bytes(32, "little"), out) == -1, Rb.hex()
 
 
 N8L = 8 * L
@@ -316,28 +380,6 @@ def test_half_scalars_lattice_reduction():
         lens.append(max(a.bit_length(), abs(b).bit_length()))
     rand = sorted(lens[len(edge):])
     assert rand[len(rand) // 2] <= 128 and rand[-1] <= 142, (rand[len(rand) // 2], rand[-1])
-
-
-def test_recode_bscalar_digit_pairs():
-    """B-scalar digit pairs: s = sum d_lo,k 2^(bbits k) + 2^bsplit sum d_hi,k
-    2^(bbits k), |d| <= 2^(bbits-1) (indexes the 0..2^(bbits-1) tables), top
-    digits >= 0 (s_hi's top one read unsigned, as the main kernel reads it)."""
-    hc = hostcheck_lib.load()
-    lay = hostcheck_lib.layout()
-    bb, split, nd = lay["bbits"], lay["bsplit"], lay["bdigits"]
-    r = random.Random(22)
-    out = (ctypes.c_uint32 * nd)()
-    vals = [0, 1, L - 1, 2**split - 1, 2**split, 2**252, 2**(split - 1) + 2**(split - 2)]
-    vals += [(2**(bb * k) - 1) % L for k in range(1, 16)] + [(2**split - 1) * k % L for k in (1, 3, 7)]
-    vals += [r.randrange(L) for _ in range(3000)]
-    for s in vals:
-        hc.hc_recode_bscalar(s.to_bytes(32, "little"), out)
-        lo = [((w & 0xffff) ^ 0x8000) - 0x8000 for w in out]
-        hi = [((w >> 16) ^ 0x8000) - 0x8000 for w in out[:-1]] + [out[-1] >> 16]
-        assert all(abs(d) <= 2**(bb - 1) for d in lo + hi), hex(s)
-        assert lo[-1] >= 0 and hi[-1] >= 0
-        v = sum(d << (bb * k) for k, d in enumerate(lo)) + (sum(d << (bb * k) for k, d in enumerate(hi)) << split)
-        assert v == s, hex(s)
 
 
 def test_kernel_algorithm_on_cpu_matches_libsodium_corpus_slice():

@@ -103,7 +103,7 @@ def parse(args):
         h2d = [e for e in es if e[2] == "h2d"]
         d2h = [e for e in es if e[2] == "d2h"]
         ks = [e for e in es if e[2].startswith("kernel:")]
-        if not h2d or not d2h or not ks:
+        if not h2d or not ks:
             continue
         add("call", t1 - t0)
         add("host_before_first_copy", h2d[0][0] - t0)
@@ -115,9 +115,12 @@ def parse(args):
             add("k%d_%s_start_after_first_copy" % (j, e[2][7:]), e[0] - h2d[0][0])
             add("k%d_%s_ms" % (j, e[2][7:]), e[1] - e[0])
         add("last_h2d_end_to_last_kernel_start", ks[-1][0] - max(e[1] for e in h2d))
-        add("last_kernel_end_to_d2h_start", d2h[-1][0] - ks[-1][1])
-        add("d2h_ms", d2h[-1][1] - d2h[-1][0])
-        add("d2h_end_to_return", t1 - d2h[-1][1])
+        if d2h:
+            add("last_kernel_end_to_d2h_start", d2h[-1][0] - ks[-1][1])
+            add("d2h_ms", d2h[-1][1] - d2h[-1][0])
+            add("d2h_end_to_return", t1 - d2h[-1][1])
+        else:  # verdicts written zero-copy by the main kernel
+            add("last_kernel_end_to_return", t1 - ks[-1][1])
         for a in api:
             if t0 <= a[0] <= t1:
                 add("api:" + a[2], a[1] - a[0])
