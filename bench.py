@@ -938,7 +938,6 @@ def main():
                      "one_gpu_same_workload_what": "rank 0's shard (%d requests per step) timed alone, %d steps, the "
                                                    "other ranks idle at a barrier, before the joint repetitions"
                                                    % (n, args.steps),
-                     "scaling_efficiency": value / (world * one_gpu),
                      "gathered_bytes": gathered_bytes,
                      "gathered": "accept bitmask, %d bytes from %d ranks (packed on each GPU, D2H, loopback TCP to "
                                  "rank 0, after the timed region)" % (gathered_bytes, world),

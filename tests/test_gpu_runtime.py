@@ -659,7 +659,7 @@ def test_bench_two_gpus_launched_by_bench():
     assert len(mg["per_rank_s"]) == 2 and mg["slowest_rank"] in (0, 1)
     assert mg["slowest_rank_s"] == max(mg["per_rank_s"])
     assert mg["one_gpu_same_workload_verifies_per_s"] > 1e6
-    assert abs(mg["scaling_efficiency"] - line["value"] / (2 * mg["one_gpu_same_workload_verifies_per_s"])) < 1e-9
+    assert "scaling_efficiency" not in mg  # the driver computes efficiency from the per-N values
     assert mg["gpu_isolation"].startswith("EDV_VIRTUAL_DEVICES")
 
 
@@ -713,5 +713,5 @@ def test_bench_c3_full_size_virtual_ranks(ranks):
     assert len(mg["per_rank_s"]) == ranks and mg["slowest_rank_s"] == max(mg["per_rank_s"])
     assert mg["gathered_bytes"] == 16777216 // 8
     assert mg["one_gpu_same_workload_verifies_per_s"] > 1e6
-    assert abs(mg["scaling_efficiency"] - line["value"] / (ranks * mg["one_gpu_same_workload_verifies_per_s"])) < 1e-9
+    assert "scaling_efficiency" not in mg
     assert line["value"] > 1e7
