@@ -12,13 +12,15 @@ namespace edv {
 namespace {
 
 // Phase 1 in three independent sides, interleaved by workgroup (block b runs
-// side side0 + b % nsides of slots [(b / nsides) 256, +256); all three by default,
-// the split pipeline launches the hash side and the two point sides apart): 0 = V2-V4 checks, V6/V7 hash,
-// half-size scalars and digits; 1 = decompress A, 0..8 x (-A) table; 2 =
-// decompress R, Q = [S]B - R, 0..8 x Q table.  They share no data, so they run side by side (three waves per
-// SIMD at 64k signatures where one kernel per side would leave one wave each
-// to hide its own latencies), and the two exponentiations no longer sit
-// behind the hash in one lane.
+// side side0 + b % nsides of slots [(b / nsides) 256, +256); all three by
+// default, the split pipeline launches the hash side and the two point sides
+// apart): 0 = V2-V4 checks, V6/V7 hash, half-size scalars and digits; 1 =
+// decompress A, 0..8 x (-A) table; 2 = decompress R, Q = [S]B - R, 0..8 x Q
+// table.  They share no data, so they run side by side (three waves per SIMD at
+// 64k signatures where one kernel per side would leave one wave each to hide
+// its own latencies), and the two exponentiations no longer sit behind the
+// hash in one lane.
+
 // The R side's view of the [S]B tables: stage() copies the lane's entry
 // straight into the wave's 10 KiB LDS slice (global_load_lds_dwordx4, 64 lanes
 // x 16 B per instruction), so the gather flies during the previous entry's
