@@ -79,29 +79,6 @@ struct GlobalATab {
     for (int q = 0; q < 10; q++) p[q] = make_int4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
   }
 };
-// The shared tables t = 0..11 of 0..2^21 x 2^(22 t) B in global memory (12 x 256
-// MiB), read as 16-byte vectors by the prep kernel's R side: one 128-byte entry
-// of each per signature.
-struct GlobalBTab {
-  const int32_t* w;
-  __device__ __forceinline__ ge_precomp entry(int tb, int j) const {
-    const int4* p = reinterpret_cast<const int4*>(w + (tb * kBEntries + j) * kBStride);
-    int32_t t[32];
-#pragma unroll
-    for (int i = 0; i < 7; i++) {
-      const int4 v = p[i];
-      t[4 * i] = v.x; t[4 * i + 1] = v.y; t[4 * i + 2] = v.z; t[4 * i + 3] = v.w;
-    }
-    // words 28, 29 only: loading the two pad words as well let the register
-    // allocator reuse their VGPRs as temporaries, which forced a vmcnt wait
-    // on the whole entry before the window's doublings (the opaque offset
-    // keeps LLVM from widening this 8-byte load back to 16 bytes)
-    const int2 v = *reinterpret_cast<const int2*>(w + (tb * kBEntries + j) * kBStride + opaque_i32(28));
-    t[28] = v.x; t[29] = v.y;
-    return precomp_from_words(t);
-  }
-};
-
 __device__ __forceinline__ void load_words(uint32_t* out, const uint32_t* p, int n4) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
