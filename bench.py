@@ -377,24 +377,28 @@ def narrow_to_own_gpu(local, world):
 
 
 # --------------------------------------------------------------- CPU baseline
-def cpu_baseline(batch, budget_s):
-    """libsodium 1.0.18 verify_detached over the same batch on the host cores
-    this process can actually use: effective_cpus = its CPU affinity capped by
-    the cgroup CPU quota (more threads than that only time-slice the same CPU
-    share).  Also the one-thread rate, and from it a labelled projection to
-    every core of the socket, which cannot be measured under the quota; plus
-    the reference's single-threaded Python chain on C1 (10k)."""
+CPU_SAMPLE = 65536   # requests of the CPU baseline's sample (the whole C2 batch; a prefix of a C3 shard)
+
+
+def cpu_baseline(arrays, budget_s, what, chain=True):
+    """libsodium 1.0.18 verify_detached over the same requests the GPU verified
+    (`arrays` = (sigs, pks, msgs, off, expected), `what` says which) on the host
+    cores this process can actually use: effective_cpus = its CPU affinity
+    capped by the cgroup CPU quota (more threads than that only time-slice the
+    same CPU share).  Also the one-thread rate, and from it a labelled
+    projection to every core of the socket, which cannot be measured under the
+    quota; plus (chain) the reference's single-threaded Python chain on C1."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as orc  # the baseline leg is the only oracle/ user here
     sb = orc.sodium_batch()
     if sb is None:
         return None
-    sigs, pks, msgs, off = batch.host_copy()
+    sigs, pks, msgs, off, expected = arrays
     info = cpu_info()
     eff = info["effective_cpus"]
-    n = batch.n
+    n = len(off) - 1
     acc = orc.sodium_verify_batch(sigs, pks, msgs, off, eff)  # warm + sanity
-    assert np.array_equal(acc, batch.expected())
+    assert np.array_equal(acc, expected), "libsodium and the construction disagree on the CPU sample"
 
     def rate(threads, seconds, k=n):
         done, t0 = 0, time.perf_counter()
@@ -410,10 +414,10 @@ def cpu_baseline(batch, budget_s):
     v_one, p_one, t_one = rate(1, max(2.0, budget_s / 4), k1)
     nproc = info["nproc"] or eff
     out = {"value": v_eff, "unit": "verifies/s", "cores": eff, "kind": "reference",
-           "sample": "%d passes over the %d-request batch (%d B msgs): libsodium %s crypto_sign_ed25519_verify_detached "
+           "sample": "%d passes over %d requests (%s, %d B msgs): libsodium %s crypto_sign_ed25519_verify_detached "
                      "(oracle/sodium_batch.c) on %d threads = the CPUs this process can use (affinity %s, cgroup "
-                     "quota %s CPUs), %.1f s"
-                     % (p_eff, n, int(off[1] - off[0]), sb.sb_version().decode(), eff, info["affinity_cpus"],
+                     "quota %s CPUs), %.1f s; verdicts equal the GPU's construction"
+                     % (p_eff, n, what, int(off[1] - off[0]), sb.sb_version().decode(), eff, info["affinity_cpus"],
                         info["cgroup_cpu_quota"], t_eff),
            "per_core_verifies_per_s": v_one,
            "per_core_sample": "1 thread, %d passes over the first %d requests, %.1f s" % (p_one, k1, t_one),
@@ -421,10 +425,11 @@ def cpu_baseline(batch, budget_s):
            "full_socket_projection_note": "projection, not measurable under the quota: per-core rate x nproc (%d)"
                                           % nproc,
            "host": info}
-    try:
-        out["c1_python_chain"] = c1_chain()
-    except Exception as ex:  # the chain needs libsodium via ctypes; report why it is missing
-        out["c1_python_chain"] = {"error": repr(ex)}
+    if chain:
+        try:
+            out["c1_python_chain"] = c1_chain()
+        except Exception as ex:  # the chain needs libsodium via ctypes; report why it is missing
+            out["c1_python_chain"] = {"error": repr(ex)}
     return out
 
 
@@ -607,6 +612,56 @@ def single_call_leg(calls=200):
         out["note"] = ("a GPU batch of one pays a whole launch pair's latency (one serial chain per lane); "
                        "callers verify per prod (INTEGRATION.md way 3), where one call carries hundreds of requests")
     return out
+
+
+NODE_PROD = 400   # requests in a Node-sized batch (a prod at C5's load)
+
+
+def footprint_child(path):
+    """Child process of footprint_leg: a fresh process (no HIP runtime loaded
+    yet) verifies the Node-sized batch in `path` through edv_verify_batch and
+    reports the first call's latency (runtime init + context creation + table
+    build + the verify), the warm latency and the library's device memory."""
+    d = np.load(path)
+    t0 = time.perf_counter()
+    from indy_plenum_amd import edv
+    edv.lib()
+    t1 = time.perf_counter()
+    acc = edv.verify_arrays(d["sigs"], d["pks"], d["msgs"], d["off"])
+    t2 = time.perf_counter()
+    assert np.array_equal(acc, d["expected"]), "cold-start call verdicts differ"
+    mem = edv.context_memory(0)
+    warm = median_time(lambda: edv.verify_arrays(d["sigs"], d["pks"], d["msgs"], d["off"]), 20)
+    print(json.dumps({"load_library_ms": 1e3 * (t1 - t0), "first_call_ms": 1e3 * (t2 - t1),
+                      "warm_call_ms": 1e3 * warm, "context_memory": mem}), flush=True)
+
+
+def footprint_leg(batch, dev):
+    """what a Node process costs a GPU.  A fresh process
+    verifies one Node-sized batch (NODE_PROD requests, host buffers, the
+    synchronous C-ABI): first-call latency with the HIP runtime and device
+    context created inside it, warm latency, and the library's device memory
+    afterwards (edv_context_memory, by kind); beside it, this bench process's
+    own footprint after the C2 legs (large [S]B tables, 2^16-request scratch)."""
+    arrays = batch.host_prefix(NODE_PROD)
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "prod.npz")
+        np.savez(path, sigs=arrays[0], pks=arrays[1], msgs=arrays[2], off=arrays[3], expected=arrays[4])
+        env = dict(os.environ)
+        if "HIP_VISIBLE_DEVICES" not in env and dev:
+            env["HIP_VISIBLE_DEVICES"] = str(dev)
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--footprint-child", path], env=env,
+                           capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        return {"error": "child rc %d: %s" % (r.returncode, r.stderr[-400:])}
+    child = json.loads(r.stdout.strip().splitlines()[-1])
+    from indy_plenum_amd import edv
+    return {"what": "a fresh process verifying one %d-request batch (256 B msgs) through edv_verify_batch: "
+                    "first call = HIP runtime + device context + [S]B table build + the verify" % NODE_PROD,
+            "node_process": child,
+            "node_process_total_mib": child["context_memory"]["total"] / 2**20,
+            "this_process_after_c2_legs": edv.context_memory(dev),
+            "table_policy": os.environ.get("EDV_SB_TABLES", "auto")}
 
 
 class DictState:
@@ -812,6 +867,7 @@ def parse_args():
     ap.add_argument("--spawn", action="store_true", help="launch the ranks from this process even for one GPU")
     ap.add_argument("--pipeline", action="store_true",
                     help="time the two-stream pipelined submission (prep of step k+1 beside main of step k)")
+    ap.add_argument("--footprint-child", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--split-prep", action="store_true",
                     help="with --pipeline: only the hash side of step k+1 beside main of step k, the point sides "
                          "after it (EDV_FLAG_SPLIT_PREP)")
@@ -820,6 +876,8 @@ def parse_args():
 
 def main():
     args = parse_args()
+    if args.footprint_child:
+        return footprint_child(args.footprint_child)
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.spawn):
         sys.exit(launch_ranks(args.gpus))
     world, rank, local, token = rank_env()
@@ -915,10 +973,17 @@ def main():
     path_ms = prep_ms + main_ms
     ops = w_total(args.msg_len) * pn
     achieved = ops / (path_ms * 1e-3)
+    # SURVEY 8d's whole-job fraction: the job's verifies/s x W(m) over N GPUs' peak
+    # (includes step gaps, rank imbalance; the kernel fraction above does not)
+    job_frac = value * w_total(args.msg_len) / (world * PEAK_INT32)
     pmc, why = pmc_figures(["edv_prep_kernel", "edv_main_kernel"], n, args.msg_len, path_ms)
     roofline = {"bound": "valu_int32", "kernel": "edv_prep_kernel + edv_main_kernel (the verify path, one launch each)",
                 "achieved": achieved / 1e12, "peak": PEAK_INT32 / 1e12, "unit": "TOP/s",
-                "frac": achieved / PEAK_INT32, "traffic": None, "traffic_unit": "bytes/launch pair",
+                "frac": achieved / PEAK_INT32, "rank0_kernel_frac": achieved / PEAK_INT32,
+                "job_frac": job_frac,
+                "job_frac_what": "value x W(m) / (n_gpus x peak): the whole job's verifies/s, step gaps and the slowest "
+                                 "rank included (SURVEY.md 8d)",
+                "traffic": None, "traffic_unit": "bytes/launch pair",
                 "traffic_source": why, "algorithmic_bytes": (64 + 32 + args.msg_len + 8 + 1) * pn,
                 "ops_per_launch": ops, "kernel_ms": path_ms, "prep_kernel_ms": prep_ms, "main_kernel_ms": main_ms,
                 "vop2_issue_peak": PEAK_VOP2 / 1e12,
@@ -1002,8 +1067,19 @@ def main():
                 out[name] = leg()
             except Exception as ex:
                 out[name] = {"error": repr(ex)}
-    if world == 1 and not c3 and not args.no_cpu_baseline:
-        cb = cpu_baseline(batch, args.cpu_seconds)
+    if world == 1 and not c3 and not args.no_e2e:
+        try:
+            out["footprint"] = footprint_leg(batch, dev)
+        except Exception as ex:
+            out["footprint"] = {"error": repr(ex)}
+    if not args.no_cpu_baseline:
+        # rank 0, after the timed region and the gather (the other ranks have
+        # left), on a bounded sample of the requests the GPUs verified: the
+        # whole C2 batch, or the first CPU_SAMPLE requests of rank 0's C3 shard
+        k = min(n, CPU_SAMPLE)
+        what = ("the C2 batch" if not c3 else
+                "the first %d requests of rank 0's C3 shard (5 %% damaged)" % k)
+        cb = cpu_baseline(batch.host_prefix(k), args.cpu_seconds, what, chain=(world == 1 and not c3))
         out["cpu_baseline"] = cb
         if cb:
             out["gpu_over_cpu"] = value / cb["value"]

@@ -42,13 +42,15 @@ extern "C" {
 
 /*
  * Verify n detached signatures held in HOST memory; synchronous.
- * A device's shard of up to one chunk (2^18 requests, edv_set_chunk) is one
- * sub-batch: H2D copies, kernels, D2H of the verdicts; a larger shard alternates
- * two streams of half-chunk sub-batches, so the copies of one overlap the
- * kernels of the other.  Inputs in pinned memory (e.g. from
- * edv_host_alloc) are copied to the device directly; pageable inputs are first
- * staged through the library's pinned buffers by a parallel memcpy
- * (EDV_COPY_THREADS threads, default 8).
+ * A device's shard of up to one chunk (2^18 requests, edv_set_chunk) is
+ * copied field by field: signatures, keys and offsets first (the point sides
+ * of the prep kernel start on them), then the messages (their hash side
+ * starts as each slice lands), then the main kernel, which writes the
+ * verdicts straight into page-locked host memory (no D2H copy).  A larger
+ * shard alternates two streams of half-chunk sub-batches, so the copies of
+ * one overlap the kernels of the other.  Inputs in pinned memory (e.g. from edv_host_alloc) are copied to the device
+ * directly; pageable inputs are first staged through the library's pinned
+ * buffers by a parallel memcpy (EDV_COPY_THREADS threads, default 8).
  *   sigs     n x 64 bytes (R || S), contiguous
  *   pks      n x 32 bytes (A), contiguous
  *   msgs     concatenated messages; message i = msgs[msg_off[i] .. msg_off[i+1])
@@ -146,10 +148,11 @@ int edv_sha256_batch_dev(const uint8_t *d_msgs, const uint64_t *d_msg_off, uint6
  * client batches, e.g. one per Node prod): enqueues the batch and returns
  * without waiting.  Consecutive submissions alternate between two internal
  * state sets, with the prep kernel (checks, decompression, SHA-512, table) of
- * batch k+1 on one library stream and the main kernel (scalar multiplication,
- * encode) of batch k on another, so both can run on the SIMDs at once
- * (measured on MI355X at C2 it is slower than sequential batches, 87.6 M
- * against 90.5 M verifies/s: profiles/r02/ab_pipeline_s30.jsonl).  Work
+ * batch k+1 on one library stream and the main kernel (the joint walk) of
+ * batch k on another, so both can run on the SIMDs at once (measured on
+ * MI355X at C2 after round 5's kernels it is slower than sequential batches,
+ * 91.8-92.3 M against 98.3-98.6 M verifies/s: profiles/r05/ab_modes_s16.jsonl;
+ * with EDV_FLAG_SPLIT_PREP it pays at C4's long messages).  Work
  * already queued on the library stream (edv_stream) is ordered before the
  * batch; inputs must stay unchanged and each batch's d_accept must not be
  * reused or read until edv_pipeline_sync(device) returns.  Same verdicts as
@@ -161,36 +164,8 @@ int edv_verify_batch_dev_pipelined(const uint8_t *d_sigs, const uint8_t *d_pks, 
 /* Wait until every pipelined batch submitted on `device` has its verdicts. */
 int edv_pipeline_sync(int device);
 
-/*
- * Measurement helper for bench.py: launches the verify kernel `iters` times
- * on device-resident inputs between two HIP events recorded on the kernel's
- * own stream and returns the elapsed milliseconds of the whole region.
- */
-int edv_time_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
-                       const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept, int device,
-                       int iters, float *ms_out);
-
-/*
- * Measurement helper: average per-launch milliseconds of the two kernels of
- * one batch (n <= chunk), each bracketed by HIP events on the kernel's stream:
- * prep (checks, decompression, SHA-512, table) and main (scalar mult, encode).
- * The length-bucketing pass runs before each pair, outside the events.
- */
-int edv_profile_batch_dev(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
-                          const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept, int device,
-                          int iters, float *ms_prep, float *ms_main);
-
-/*
- * Measurement helper: edv_profile_batch_dev with, when flush_bytes > 0, a
- * kernel between prep and main that reads and rewrites a flush_bytes buffer
- * (larger than the 256 MiB Infinity Cache: the prep kernel's tables are
- * evicted before main reads them); ms_flush = that kernel's time.  Tells the
- * main kernel's DRAM sensitivity apart from its Infinity-Cache hits.
- */
-int edv_profile_batch_dev_flush(const uint8_t *d_sigs, const uint8_t *d_pks, const uint8_t *d_msgs,
-                                const uint64_t *d_msg_off, uint64_t msg_base, uint64_t n, uint8_t *d_accept,
-                                int device, int iters, uint64_t flush_bytes, float *ms_prep, float *ms_flush,
-                                float *ms_main);
+/* (Kernel timing and fault injection are not part of this ABI: they live in
+ * the benchmark build libedv_measure.so, include/edv_measure.h.) */
 
 /* Signatures per prep/main kernel pair on `device` (0 = default 2^18; rounded
  * down to a multiple of 256).  Tuning/testing knob: verdicts never depend on it. */
@@ -264,6 +239,20 @@ int edv_pick_device(uint32_t device_mask);
  */
 int edv_pack_bits_dev(const uint8_t *d_accept, uint64_t n, uint8_t *d_bits, int device, void *stream);
 int edv_context_count(void);
+
+/*
+ * Device memory the library holds for `device` in this process, in bytes:
+ * out[0] total, out[1] the [S]B tables (shared by the logical devices of one
+ * GPU), out[2] chunk scratch of the ordinary paths, out[3] the asynchronous
+ * slots (inputs and small-batch scratch), out[4] the pipelined state sets,
+ * out[5] input buffers of the synchronous path, out[6] the signer's comb
+ * table.  Scratch grows with the largest batch seen (up to one chunk), so a
+ * Node that verifies prods of a few hundred requests holds a few hundred MB;
+ * 0 for a device whose context does not exist yet.  (What a Node process
+ * costs a GPU it shares with other Node processes: scripts/start_plenum_node
+ * runs one Node per process.)
+ */
+int edv_context_memory(int device, uint64_t out[7]);
 
 /*
  * The shard split edv_verify_batch uses (host only, no GPU needed): bounds[0..g]

@@ -21,13 +21,15 @@ struct HostATab {
   void stage(int e) { staged = e; }
   ge_cached fetch() const { return t[staged]; }
 };
-// The R side's view of the [S]B tables: each entry computed when asked for, by
-// the device table's own btab_entry (the 16 x 32,769 entries would take a
-// minute to build on one core; a verify needs 16 of them).
+// The R side's view of an [S]B table set (large or compact): each entry
+// computed when asked for, by the device table's own btab_entry (the sets'
+// millions of entries would take minutes to build on one core; a verify needs
+// 12 or 16 of them).
 struct HostBTab {
-  ge_p3 base[kBTables];
-  HostBTab() {
-    for (int t = 0; t < kBTables; t++) base[t] = base_point(t * kBBits);
+  SbShape sh;
+  ge_p3 base[kBTablesCompact];
+  explicit HostBTab(SbShape s) : sh(s) {
+    for (int t = 0; t < sh.tables; t++) base[t] = base_point(t * sh.bits);
   }
   ge_precomp entry(int t, int j) const {
     int32_t w[kBStride];
@@ -39,6 +41,7 @@ struct HostBStage {
   const HostBTab& b;
   int t = 0, j = 0;
   ge_cached stash;
+  SbShape shape() const { return b.sh; }
   void stage(int tt, int jj) { t = tt; j = jj; }
   ge_precomp fetch() const { return b.entry(t, j); }
   void put(const ge_cached& c) { stash = c; }
@@ -56,9 +59,10 @@ const HostComb& comb() {
   static HostComb c;
   return c;
 }
-const HostBTab& btab() {
-  static HostBTab b;
-  return b;
+static_assert(kBTablesCompact >= kBTables, "base[] holds the larger table count");
+const HostBTab& btab(int bits = kBBits) {
+  static HostBTab large(sb_large()), compact(sb_compact());
+  return bits == kBBitsCompact ? compact : large;
 }
 void load_words(uint32_t* w, const uint8_t* b, int n) {
   for (int i = 0; i < n; i++) w[i] = uint32_t(b[4 * i]) | uint32_t(b[4 * i + 1]) << 8 | uint32_t(b[4 * i + 2]) << 16 | uint32_t(b[4 * i + 3]) << 24;
@@ -128,17 +132,24 @@ int hc_sha256_batch(const uint8_t* msgs, const uint64_t* off, uint64_t n, uint8_
   }
   return 0;
 }
-// entries js[0..nj) of table t (j x 2^(kBBits t) B), kBStride words each
-int hc_btab_entries_of(int t, const int32_t* js, int nj, int32_t* out) {
-  if (t < 0 || t >= kBTables) return -1;
+// entries js[0..nj) of table t (j x 2^(bits t) B) of the set with `bits`
+// (22 large, 16 compact), kBStride words each
+int hc_btab_entries_of_bits(int bits, int t, const int32_t* js, int nj, int32_t* out) {
+  if (bits != kBBits && bits != kBBitsCompact) return -1;
+  const HostBTab& b = btab(bits);
+  if (t < 0 || t >= b.sh.tables) return -1;
   for (int k = 0; k < nj; k++) {
-    if (js[k] < 0 || js[k] >= kBEntries) return -1;
-    btab_entry(out + size_t(k) * kBStride, js[k], btab().base[t]);
+    if (js[k] < 0 || js[k] >= b.sh.entries) return -1;
+    btab_entry(out + size_t(k) * kBStride, js[k], b.base[t]);
   }
   return 0;
 }
-// the R side's Q = [S]B - R, encoded (0), or -1 if R is rejected
-int hc_rside_point(const uint8_t* R32, const uint8_t* S32, uint8_t* out32) {
+int hc_btab_entries_of(int t, const int32_t* js, int nj, int32_t* out) {
+  return hc_btab_entries_of_bits(kBBits, t, js, nj, out);
+}
+// the R side's Q = [S]B - R against the table set with `bits`, encoded (0),
+// or -1 if R is rejected
+int hc_rside_point_bits(int bits, const uint8_t* R32, const uint8_t* S32, uint8_t* out32) {
   struct Keep {  // keeps entry 1 of the table: Q itself
     ge_cached q;
     void store(int e, const ge_cached& c) { if (e == 1) q = c; }
@@ -146,7 +157,8 @@ int hc_rside_point(const uint8_t* R32, const uint8_t* S32, uint8_t* out32) {
   uint32_t R[8], S[8], o[8];
   load_words(R, R32, 8);
   load_words(S, S32, 8);
-  HostBStage bs{btab()};
+  if (bits != kBBits && bits != kBBitsCompact) return -1;
+  HostBStage bs{btab(bits)};
   if (!prep_rpoint(R, S, tab, bs)) return -1;
   // cached (Y+X, Y-X, Z, 2dT) -> (X : Y : Z)
   const fe two_y = fe_carry32(fe_add(tab.q.YpX, tab.q.YmX)), two_x = fe_carry32(fe_sub(tab.q.YpX, tab.q.YmX));
@@ -154,6 +166,9 @@ int hc_rside_point(const uint8_t* R32, const uint8_t* S32, uint8_t* out32) {
   ge_p2_tobytes(o, p);
   store_words(out32, o, 8);
   return 0;
+}
+int hc_rside_point(const uint8_t* R32, const uint8_t* S32, uint8_t* out32) {
+  return hc_rside_point_bits(kBBits, R32, S32, out32);
 }
 // the lattice reduction of the prep kernel: (a, u, neg) for h (32-byte scalars)
 int hc_half_scalars(const uint8_t* h32, uint8_t* a32, uint8_t* u32) {

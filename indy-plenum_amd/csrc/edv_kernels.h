@@ -50,7 +50,8 @@ struct VerifyArgs {
   uint64_t n;             // signatures in this chunk
   uint8_t* accept;        // indexed by global signature index
   ChunkState st;
-  const int32_t* btab;    // kBTables x kBEntries x kBStride (the prep kernel's R side)
+  const int32_t* btab;    // sb.tables x sb.entries x kBStride (the prep kernel's R side)
+  SbShape sb;             // which [S]B table set btab is (large or compact, edv_verify_core.h)
   // prep sides this launch runs: workgroup b runs side side0 + b % nsides
   // (0 hash, 1 A, 2 R); 0 / 3 = all three, 0 / 1 = the hash side, 1 / 2 = the points
   int32_t side0;
@@ -88,7 +89,10 @@ __device__ __forceinline__ void load_words(uint32_t* out, const uint32_t* p, int
   }
 }
 
-// Launches edv_prep_kernel (edv_prep.hip) over `grid` workgroups on stream s.
+// Launches edv_prep_kernel (edv_prep.hip) over `grid` workgroups on stream s;
+// the R side's LDS staging is dynamic shared memory, reserved only by launches
+// that run the R side (a hash-side or A-side launch is not capped at four
+// workgroups per CU by 40 KiB it never touches).
 hipError_t launch_prep_kernel(unsigned grid, hipStream_t s, const VerifyArgs& va);
 
 }  // namespace edv

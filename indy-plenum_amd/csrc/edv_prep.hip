@@ -30,12 +30,17 @@ constexpr int kBPieces = 8;         // 128-byte entry (30 words used)
 constexpr int kStashPieces = 10;    // cached point, 160 B
 __device__ __forceinline__ void wait_staged() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// BITS: the table set (a compile-time shape: with the shape read at run time
+// the R side's loop kept ~90 more dwords spilled, prep +7 %)
+template <int BITS>
 struct LdsBStage {
   const int32_t* w;  // the shared tables
   int32_t* lds;      // the wave's slice: kStashPieces x 64 lanes x 4 words
   int lane;
+  static constexpr SbShape kShape = BITS == kBBits ? sb_large() : sb_compact();
+  __device__ __forceinline__ SbShape shape() const { return kShape; }
   __device__ __forceinline__ void stage(int t, int j) {
-    const int32_t* g = w + (size_t(t) * kBEntries + j) * kBStride;
+    const int32_t* g = w + (size_t(t) * kShape.entries + j) * kBStride;
 #pragma unroll
     for (int q = 0; q < kBPieces; q++)
       __builtin_amdgcn_global_load_lds(const_cast<int32_t*>(g + 4 * q), lds + q * 256, 16, 0, 0);
@@ -75,6 +80,7 @@ struct LdsBStage {
 };
 constexpr int kLdsBWaveWords = kStashPieces * 256;
 
+template <int BITS>
 __device__ __forceinline__ void prep_point_side(const VerifyArgs& a, uint64_t j, int side, int32_t* lds) {
   if (j >= a.n) return;
   const uint64_t i = a.base + (a.st.perm ? a.st.perm[j] : j);
@@ -89,21 +95,20 @@ __device__ __forceinline__ void prep_point_side(const VerifyArgs& a, uint64_t j,
     load_words(P, a.sigs + 16 * i, 2);
     load_words(S, a.sigs + 16 * i + 8, 2);
     GlobalATab tab{a.st.rtab + j * kAWords};
-    LdsBStage bs{a.btab, lds + (threadIdx.x >> 6) * kLdsBWaveWords, int(threadIdx.x & 63)};
+    LdsBStage<BITS> bs{a.btab, lds + (threadIdx.x >> 6) * kLdsBWaveWords, int(threadIdx.x & 63)};
     ok = prep_rpoint(P, S, tab, bs);
   }
   a.st.alive[side * a.st.cap + j] = ok ? 1 : 0;
   if (!ok) a.accept[i] = 0;
 }
-// the register budget allows at least three waves per SIMD (the three sides)
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void edv_prep_kernel(
-    VerifyArgs a) {
-  __shared__ int32_t lds_b[(kBlock / 64) * kLdsBWaveWords];
+// The kernel body for table set BITS (one kernel per set, below).
+template <int BITS>
+__device__ __forceinline__ void prep_body(const VerifyArgs& a, int32_t* lds_b) {
   const uint32_t ns = uint32_t(a.nsides);
   const int side = a.side0 + int(blockIdx.x % ns);
   const uint64_t j = uint64_t(blockIdx.x / ns) * kBlock + threadIdx.x;  // slot within the chunk
   if (side != 0) {
-    prep_point_side(a, j, side, lds_b);
+    prep_point_side<BITS>(a, j, side, lds_b);
     return;
   }
   if (j >= a.n) return;
@@ -130,10 +135,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
   }
 }
 
+// the register budget allows at least three waves per SIMD (the three sides);
+// the R side's LDS staging, (kBlock / 64) * kLdsBWaveWords words, is dynamic
+// shared memory that only launches running the R side reserve
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void edv_prep_kernel(
+    VerifyArgs a) {
+  extern __shared__ int32_t lds_b[];
+  prep_body<kBBits>(a, lds_b);
+}
+// the same against the compact [S]B tables (edv_verify_core.h SbShape)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void edv_prep_kernel_compact(
+    VerifyArgs a) {
+  extern __shared__ int32_t lds_b[];
+  prep_body<kBBitsCompact>(a, lds_b);
+}
+
 }  // namespace
 
 hipError_t launch_prep_kernel(unsigned grid, hipStream_t s, const VerifyArgs& va) {
-  edv_prep_kernel<<<dim3(grid), dim3(kBlock), 0, s>>>(va);
+  const bool rside = va.side0 + va.nsides > 2;  // sides side0 .. side0 + nsides - 1 include side 2
+  const size_t lds = rside ? size_t(kBlock / 64) * kLdsBWaveWords * sizeof(int32_t) : 0;
+  if (va.sb.bits == kBBits) edv_prep_kernel<<<dim3(grid), dim3(kBlock), lds, s>>>(va);
+  else edv_prep_kernel_compact<<<dim3(grid), dim3(kBlock), lds, s>>>(va);
   return hipGetLastError();
 }
 

@@ -41,19 +41,6 @@ int set_err(int code, const char* what, hipError_t e = hipSuccess) {
     if (e_ != hipSuccess) return set_err(EDV_E_HIP, what, e_); \
   } while (0)
 
-// HIP events of a measurement helper, destroyed on every return path
-struct Events {
-  hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
-  int n = 0;
-  int create(int k) {
-    for (n = 0; n < k; n++) HIPOK(hipEventCreate(&e[n]), "event");
-    return 0;
-  }
-  ~Events() {
-    for (int i = 0; i < n; i++) (void)hipEventDestroy(e[i]);
-  }
-};
-
 struct DevBuf {
   void* p = nullptr;
   uint64_t cap = 0;
@@ -107,17 +94,31 @@ constexpr int kAsyncSlots = 8;
 // walk, ~0.45 ms) is all it costs.  Larger batches share the chunk scratch.
 constexpr uint64_t kSmallAsync = 8192;
 
-// One set of per-chunk state buffers (ChunkState storage + bucket permutation).
+// One set of per-chunk state buffers (ChunkState storage + bucket permutation)
+// for `cap` signatures (~5.5 kB each: ~1.4 GB for a whole 2^18 chunk).  Sized
+// by use, not up front: a set grows to the largest batch it has served (in
+// steps of powers of two from 4,096, at most the chunk), so a Node verifying
+// prods of a few hundred requests holds ~25 MB of it, not 1.4 GB.  The caller
+// guarantees that no queued kernel still uses a set it grows (grow_state).
 struct ChunkBufs {
-  DevBuf atab, rtab, dig, alive;  // ChunkState storage for `chunk` signatures (~1.4 GB at 2^18)
+  DevBuf atab, rtab, dig, alive;  // ChunkState storage
   DevBuf perm, bucket_ctr;  // length-bucket permutation of a chunk; histogram + cursors (one set per stream)
-  int ensure(uint64_t chunk) {
-    if (atab.ensure(chunk * kAWords * 4) || rtab.ensure(chunk * kAWords * 4) || dig.ensure(chunk * kDigWords * 4) ||
-        alive.ensure(3 * chunk) ||
-        perm.ensure(chunk * 4) || bucket_ctr.ensure(uint64_t(kQ) * 2 * kBuckets * 4))
+  uint64_t cap = 0;         // signatures the set holds (the row stride of dig / alive)
+  bool fits(uint64_t need) const { return need <= cap; }
+  int ensure(uint64_t need, uint64_t limit) {
+    if (need <= cap) return 0;
+    uint64_t c = 4096;
+    while (c < need) c <<= 1;
+    if (c > limit) c = limit > need ? limit : need;
+    if (atab.ensure(c * kAWords * 4) || rtab.ensure(c * kAWords * 4) || dig.ensure(c * kDigWords * 4) ||
+        alive.ensure(3 * c) || perm.ensure(c * 4) || bucket_ctr.ensure(uint64_t(kQ) * 2 * kBuckets * 4)) {
+      cap = 0;
       return EDV_E_OOM;
+    }
+    cap = c;
     return 0;
   }
+  uint64_t bytes() const { return atab.cap + rtab.cap + dig.cap + alive.cap + perm.cap + bucket_ctr.cap; }
 };
 
 struct DevCtx {
@@ -128,8 +129,8 @@ struct DevCtx {
   int dev = -1;                    // logical device (edv_* device index)
   int phys = -1;                   // HIP device it runs on
   hipStream_t stream = nullptr;    // the library stream (edv_stream)
-  int32_t* btab = nullptr;
-  bool btab_built = false;
+  const int32_t* sb_compact = nullptr;  // the GPU's [S]B table sets (shared_tables), when built
+  const int32_t* sb_large = nullptr;
   int32_t* comb = nullptr;         // signer comb table, built on first edv_sign_* call
   uint64_t chunk = kChunkDefault;  // EDV_CHUNK overrides (tests exercise chunk seams)
   int length_buckets = 2;          // 0 never, 1 always, 2 auto (edv_set_length_buckets)
@@ -161,7 +162,10 @@ struct DevCtx {
     bool acc_pinned = false;     // verdicts DMA'd straight into `accept`
     bool dig_pinned = false;     // digests DMA'd straight into `digests`
     hipStream_t st = nullptr;    // small batches: copies, kernels and D2H all on this stream
-    ChunkBufs cb;                // small batches: the slot's own chunk scratch (kSmallAsync)
+    ChunkBufs cb;                // small batches: the slot's own chunk scratch (grown to the batch)
+#ifdef EDV_MEASUREMENT_API
+    bool injected = false;       // edv_test_fail_async: this batch launched nothing and fails
+#endif
   };
   AsyncSlot as[kAsyncSlots];
   hipStream_t hac = nullptr;
@@ -182,11 +186,75 @@ struct DevCtx {
   hipEvent_t perm_done[2] = {nullptr, nullptr};  // split prep: state set b's bucket permutation is written
   bool pending[2] = {false, false};
   int next = 0;
+#ifdef EDV_MEASUREMENT_API
+  int64_t inject_fail = -1;        // edv_test_fail_async (libedv_measure.so only)
+#endif
 };
 
 std::mutex g_mu;
 std::vector<DevCtx*> g_ctx;
 int g_ndev = -1;
+
+// ---- the [S]B tables (the prep kernel's R side): one copy per GPU and shape
+// in a process, shared by every logical device (EDV_VIRTUAL_DEVICES) mapped
+// onto that GPU.  Which shapes a context builds (EDV_SB_TABLES):
+//   auto (default)  the compact set (64 MiB) at context creation; the large
+//                   set (3 GiB, 4 fewer additions per verify, +1 % at C2) once
+//                   a batch of at least kLargeTablesMin requests arrives -- a
+//                   Node verifying prods of a few hundred requests never
+//                   allocates it (footprint)
+//   compact         never the large set
+//   large           the large set at context creation (the compact one never)
+// A failed allocation of the large set leaves the compact one in use.
+constexpr uint64_t kLargeTablesMin = 65536;  // one wave per SIMD of a whole MI355X
+enum SbPolicy { kSbAuto, kSbCompact, kSbLarge };
+SbPolicy sb_policy() {
+  static const SbPolicy p = [] {
+    const char* e = getenv("EDV_SB_TABLES");
+    if (e && !strcmp(e, "compact")) return kSbCompact;
+    if (e && !strcmp(e, "large")) return kSbLarge;
+    return kSbAuto;
+  }();
+  return p;
+}
+struct SbSet {
+  int phys;
+  int bits;
+  int32_t* p;
+  uint64_t bytes;
+};
+std::mutex g_sb_mu;
+std::vector<SbSet> g_sb;
+// The table set of shape sh on GPU phys (current device = phys), built on
+// first use; nullptr (with the error set) if it cannot be allocated or built.
+const int32_t* shared_tables(int phys, SbShape sh, hipStream_t s, int* err) {
+  std::lock_guard<std::mutex> lk(g_sb_mu);
+  for (const SbSet& t : g_sb)
+    if (t.phys == phys && t.bits == sh.bits) return t.p;
+  const uint64_t bytes = sb_alloc_bytes(sh);
+  int32_t* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    *err = set_err(EDV_E_OOM, "hipMalloc [S]B tables");
+    return nullptr;
+  }
+  hipError_t e = launch_btab_kernel(s, p, sh);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    *err = set_err(EDV_E_HIP, "[S]B table build", e);
+    return nullptr;
+  }
+  g_sb.push_back({phys, sh.bits, p, bytes});
+  return p;
+}
+uint64_t shared_tables_bytes(int phys) {
+  std::lock_guard<std::mutex> lk(g_sb_mu);
+  uint64_t b = 0;
+  for (const SbSet& t : g_sb)
+    if (t.phys == phys) b += t.bytes;
+  return b;
+}
 
 // Logical devices.  Normally one per visible HIP device.  EDV_VIRTUAL_DEVICES=k
 // (testing knob) presents k logical devices mapped round-robin onto the
@@ -243,12 +311,12 @@ int ctx_init(DevCtx& c) {
     const uint64_t v = strtoull(e, nullptr, 10);
     if (v >= kBlock && v <= (uint64_t(1) << 24)) c.chunk = (v / kBlock) * kBlock;
   }
-  if (c.st.ensure(c.chunk)) return EDV_E_OOM;
-  if (!c.btab) HIPOK(hipMalloc(&c.btab, kBTabAllocBytes), "hipMalloc btab");
-  if (!c.btab_built) {
-    HIPOK(launch_btab_kernel(c.stream, c.btab), "btab launch");
-    HIPOK(hipStreamSynchronize(c.stream), "btab sync");
-    c.btab_built = true;
+  // the scratch grows by use (ChunkBufs); the [S]B tables: see sb_policy
+  int err = 0;
+  if (sb_policy() == kSbLarge) {
+    if (!c.sb_large && !(c.sb_large = shared_tables(c.phys, sb_large(), c.stream, &err))) return err;
+  } else if (!c.sb_compact && !(c.sb_compact = shared_tables(c.phys, sb_compact(), c.stream, &err))) {
+    return err;
   }
   c.ready = true;
   c.live.store(true);
@@ -285,9 +353,36 @@ int phys_of(int device, int* phys) {
   return 0;
 }
 
-VerifyArgs make_args(const DevCtx& c, ChunkBufs& b, const uint8_t* d_sigs, const uint8_t* d_pks,
+// The [S]B table set a batch of n requests runs against (sb_policy): the
+// large set once built (or once a batch this large asks for it), else the
+// compact one.  Caller holds c.mu; the current device is c.phys.
+void pick_tables(DevCtx& c, uint64_t n, const int32_t** t, SbShape* sh) {
+  if (!c.sb_large && sb_policy() == kSbAuto && n >= kLargeTablesMin) {
+    int err = 0;
+    c.sb_large = shared_tables(c.phys, sb_large(), c.stream, &err);  // stays compact if this fails
+    if (!c.sb_large) g_err.clear();
+  }
+  if (c.sb_large) {
+    *t = c.sb_large;
+    *sh = sb_large();
+  } else {
+    *t = c.sb_compact;
+    *sh = sb_compact();
+  }
+}
+
+// Grow the context's ordinary chunk scratch to `need` signatures (at most one
+// chunk's worth is ever used at once), after every queued user of it is done.
+int grow_state(DevCtx& c, uint64_t need) {
+  if (need > c.chunk) need = c.chunk;
+  if (c.st.fits(need)) return 0;
+  HIPOK(hipEventSynchronize(c.st_done), "scratch sync");
+  return c.st.ensure(need, c.chunk);
+}
+
+VerifyArgs make_args(DevCtx& c, ChunkBufs& b, const uint8_t* d_sigs, const uint8_t* d_pks,
                      const uint8_t* d_msgs, const uint64_t* d_off, uint64_t msg_base, uint8_t* d_accept, bool bucket,
-                     uint64_t slot0 = 0, uint64_t cap = 0) {
+                     uint64_t slot0 = 0, uint64_t batch = 0) {
   VerifyArgs va;
   va.sigs = reinterpret_cast<const uint32_t*>(d_sigs);
   va.pks = reinterpret_cast<const uint32_t*>(d_pks);
@@ -298,9 +393,9 @@ VerifyArgs make_args(const DevCtx& c, ChunkBufs& b, const uint8_t* d_sigs, const
   // slots [slot0, slot0 + n) of the chunk scratch (dig stays indexed w * cap + slot)
   va.st = ChunkState{static_cast<int32_t*>(b.atab.p) + slot0 * kAWords, static_cast<int32_t*>(b.rtab.p) + slot0 * kAWords,
                      static_cast<uint32_t*>(b.dig.p) + slot0,
-                     static_cast<uint8_t*>(b.alive.p) + slot0, cap ? cap : c.chunk,
+                     static_cast<uint8_t*>(b.alive.p) + slot0, b.cap,
                      bucket ? static_cast<uint32_t*>(b.perm.p) + slot0 : nullptr};
-  va.btab = c.btab;
+  pick_tables(c, batch, &va.btab, &va.sb);
   va.base = 0;
   va.n = 0;
   va.side0 = 0;
@@ -367,9 +462,10 @@ int launch(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t
            uint64_t msg_base, uint64_t n, uint8_t* d_accept, hipStream_t s, uint32_t flags) {
   if (n == 0) return 0;
   const bool bucket = bucketing_enabled(c, flags);
-  HIPOK(hipStreamWaitEvent(s, c.st_done, 0), "wait scratch");
-  VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, msg_base, d_accept, bucket);
   int err;
+  if ((err = grow_state(c, n))) return err;
+  HIPOK(hipStreamWaitEvent(s, c.st_done, 0), "wait scratch");
+  VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, msg_base, d_accept, bucket, 0, n);
   for (uint64_t base = 0; base < n; base += c.chunk) {
     va.base = base;
     va.n = (n - base) < c.chunk ? (n - base) : c.chunk;
@@ -379,16 +475,17 @@ int launch(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t
   return 0;
 }
 
-// A small asynchronous batch on its slot's own scratch (row stride cap) and
-// stream: no ordering against the shared scratch, so batches of different
-// slots run concurrently.  Chunks of at most c.chunk, as launch() walks them.
-int launch_own(DevCtx& c, ChunkBufs& cb, uint64_t cap, const uint8_t* d_sigs, const uint8_t* d_pks,
-               const uint8_t* d_msgs, const uint64_t* d_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept,
-               hipStream_t s, uint32_t flags) {
+// A small asynchronous batch on its slot's own scratch (cb, grown to the
+// batch by the caller once the slot's previous batch is complete) and stream:
+// no ordering against the shared scratch, so batches of different slots run
+// concurrently.  Chunks of at most c.chunk, as launch() walks them.
+int launch_own(DevCtx& c, ChunkBufs& cb, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
+               const uint64_t* d_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, hipStream_t s,
+               uint32_t flags) {
   if (n == 0) return 0;
   const bool bucket = bucketing_enabled(c, flags);
-  VerifyArgs va = make_args(c, cb, d_sigs, d_pks, d_msgs, d_off, msg_base, d_accept, bucket, 0, cap);
-  const uint64_t step = c.chunk < cap ? c.chunk : cap;
+  VerifyArgs va = make_args(c, cb, d_sigs, d_pks, d_msgs, d_off, msg_base, d_accept, bucket, 0, n);
+  const uint64_t step = c.chunk < cb.cap ? c.chunk : cb.cap;
   int err;
   for (uint64_t base = 0; base < n; base += step) {
     va.base = base;
@@ -400,7 +497,6 @@ int launch_own(DevCtx& c, ChunkBufs& cb, uint64_t cap, const uint8_t* d_sigs, co
 
 int pipe_init(DevCtx& c) {
   if (c.pipe_ready) return 0;
-  if (c.pst[0].ensure(c.chunk) || c.pst[1].ensure(c.chunk)) return EDV_E_OOM;
   if (!c.sp) HIPOK(hipStreamCreateWithFlags(&c.sp, hipStreamNonBlocking), "hipStreamCreate");
   if (!c.sm) HIPOK(hipStreamCreateWithFlags(&c.sm, hipStreamNonBlocking), "hipStreamCreate");
   for (int b = 0; b < 2; b++) {
@@ -430,9 +526,14 @@ int launch_pipelined(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, con
     const int b = c.next;
     c.next ^= 1;
     ChunkBufs& cb = c.pst[b];
-    VerifyArgs va = make_args(c, cb, d_sigs, d_pks, d_msgs, d_off, msg_base, d_accept, bucket);
+    const uint64_t cn = (n - base) < c.chunk ? (n - base) : c.chunk;
+    if (!cb.fits(cn)) {  // state set b grows: its last main kernel must be done
+      if (c.pending[b]) HIPOK(hipEventSynchronize(c.main_done[b]), "pipeline sync");
+      if (cb.ensure(cn, c.chunk)) return EDV_E_OOM;
+    }
+    VerifyArgs va = make_args(c, cb, d_sigs, d_pks, d_msgs, d_off, msg_base, d_accept, bucket, 0, n);
     va.base = base;
-    va.n = (n - base) < c.chunk ? (n - base) : c.chunk;
+    va.n = cn;
     if (c.pending[b]) HIPOK(hipStreamWaitEvent(c.sp, c.main_done[b], 0), "wait");
     if (split) {
       // Split prep: the hash side (one latency-bound SHA-512 chain per lane,
@@ -605,7 +706,16 @@ uint64_t sha512_blocks(const uint64_t* off, uint64_t i) { return (64 + (off[i + 
 struct OffScan {
   bool ok, uniform;
 };
-OffScan scan_offsets(const uint64_t* off, uint64_t lo, uint64_t hi) {
+// Built twice (target_clones): an AVX2 clone, picked at load time on hosts
+// that have it (the C2 scan in ~20 us), and the x86-64 baseline for the rest;
+// the rest of the library's host code is baseline x86-64.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define EDV_HOST_CLONES
+#else
+#define EDV_HOST_CLONES __attribute__((target_clones("avx2", "default")))
+#endif
+EDV_HOST_CLONES OffScan scan_offsets(const uint64_t* off, uint64_t lo,
+                                                                        uint64_t hi) {
   const uint64_t nb0 = sha512_blocks(off, lo);
   uint64_t bad = 0, diff = 0;
   for (uint64_t i = lo; i < hi; i++) {
@@ -641,6 +751,8 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
                      uint8_t* d_msgs, uint64_t* d_off, uint8_t* d_acc, uint8_t* h_acc) {
   const uint64_t n = hi - lo, mbase = off[lo], mbytes = off[hi] - mbase;
   const hipStream_t cp = c.hcp, s0 = c.hs[0];
+  int err;
+  if ((err = grow_state(c, n))) return err;
   // the scratch's previous users (any stream) finish before the kernels write it,
   // and the copies follow the previous call's (nothing to wait for when its
   // last user is already done, e.g. the previous synchronous call)
@@ -701,7 +813,6 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
     mb[k] = off[lo + rb[k]] - mbase;
   }
   HIPOK(hipEventRecord(c.part_copied[0], cp), "record");
-  int err;
   // The kernels write the verdicts straight into the page-locked host buffer
   // (one 64-byte PCIe write per wave), so no D2H copy and its launch gap follow
   // the main kernel (C2 pinned 1.075 -> 1.046 ms, with the in-stream hash side
@@ -711,7 +822,7 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
   else (void)hipGetLastError();
   const bool zc_acc = zc != nullptr;
   // the point sides first: they need only what has just been queued
-  VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, mbase, d_acc, bucket);
+  VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, mbase, d_acc, bucket, 0, n);
   va.n = n;
   HIPOK(hipStreamWaitEvent(s0, c.part_copied[0], 0), "wait copy");
   if (bucket && (err = launch_buckets(bucket_ctr(c.st, 0), va, d_off, s0))) return err;
@@ -818,6 +929,7 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
     return 0;
   }
   hipStream_t* hs = c.hs;
+  if ((err = grow_state(c, uint64_t(Q) * pmax))) return err;  // sub-batch stream q uses slots [q pmax, (q + 1) pmax)
   for (int q = 0; q < Q; q++) HIPOK(hipStreamWaitEvent(hs[q], c.st_done, 0), "wait scratch");
   for (uint64_t k = 0; k < nsub; k++) {
     const int q = int(k % Q);
@@ -854,7 +966,7 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
     if (!pinned) HIPOK(hipEventRecord(c.hs_staged[q], s), "record");
     const bool bucket = bucketing_enabled(c, flags);
     VerifyArgs va = make_args(c, c.st, d_sigs + 64 * (a - lo), d_pks + 32 * (a - lo), d_msgs, d_o, mbase,
-                              d_acc + (a - lo), bucket, uint64_t(q) * pmax);
+                              d_acc + (a - lo), bucket, uint64_t(q) * pmax, n);
     va.n = cnt;
     if ((err = launch_prep(bucket_ctr(c.st, q), va, d_o, bucket, s)) || (err = launch_main(va, s))) return err;
     HIPOK(hipMemcpyAsync(h_acc + (a - lo), d_acc + (a - lo), cnt, hipMemcpyDeviceToHost, s), "d2h accept");
@@ -908,6 +1020,13 @@ int async_complete(DevCtx& c, DevCtx::AsyncSlot& s) {
     async_fail(c, s);
     return set_err(EDV_E_HIP, "async wait", e);
   }
+#ifdef EDV_MEASUREMENT_API
+  if (s.injected) {
+    s.injected = false;
+    async_fail(c, s);
+    return set_err(EDV_E_HIP, "async batch failed (injected by edv_test_fail_async)");
+  }
+#endif
   if (!s.acc_pinned) memcpy(s.accept, s.acc_host.p, s.n);
   if (s.digests && !s.dig_pinned) memcpy(s.digests, s.dig_host.p, 32 * s.n);
   s.ticket = -1;
@@ -937,7 +1056,7 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
   const bool own = n <= kSmallAsync;
   if (own) {
     if (!s.st) HIPOK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking), "hipStreamCreate");
-    if (s.cb.ensure(kSmallAsync)) return EDV_E_OOM;
+    if (s.cb.ensure(n, kSmallAsync)) return EDV_E_OOM;  // the slot's previous batch is complete
   }
   const hipStream_t cs = own ? s.st : c.hcp, ks = own ? s.st : c.hac;
   s.dig_pinned = digests && is_pinned(digests);
@@ -977,11 +1096,15 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
   void* zc = nullptr;
   if (hipHostGetDevicePointer(&zc, h_acc, 0) == hipSuccess && zc) d_acc = static_cast<uint8_t*>(zc);
   else (void)hipGetLastError();
-  if ((err = own ? launch_own(c, s.cb, kSmallAsync, d_sigs, d_pks, d_msgs, d_off, mbase, n, d_acc, ks, lflags)
-                 : launch(c, d_sigs, d_pks, d_msgs, d_off, mbase, n, d_acc, ks, lflags)))
+  bool skip = false;  // edv_test_fail_async (measurement build): no kernels, and the wait fails
+#ifdef EDV_MEASUREMENT_API
+  skip = s.injected = (t == c.inject_fail);
+#endif
+  if (!skip && (err = own ? launch_own(c, s.cb, d_sigs, d_pks, d_msgs, d_off, mbase, n, d_acc, ks, lflags)
+                          : launch(c, d_sigs, d_pks, d_msgs, d_off, mbase, n, d_acc, ks, lflags)))
     return err;
   if (!zc) HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, ks), "d2h accept");
-  if (digests) {
+  if (digests && !skip) {
     // Request.getDigest of requests whose signing bytes ARE the message (the
     // caller decides which): SHA-256 of the same resident message bytes
     uint8_t* d_dig = static_cast<uint8_t*>(s.dig.p);
@@ -1220,6 +1343,26 @@ int edv_context_count(void) {
   return k;
 }
 
+int edv_context_memory(int device, uint64_t out[7]) {
+  g_err.clear();
+  if (!out) return set_err(EDV_E_ARG, "null pointer");
+  for (int k = 0; k < 7; k++) out[k] = 0;
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->ready) return 0;
+  out[1] = shared_tables_bytes(c->phys);
+  out[2] = c->st.bytes();
+  for (const auto& a : c->as)
+    out[3] += a.sigs.cap + a.pks.cap + a.msgs.cap + a.off.cap + a.acc.cap + a.dig.cap + a.cb.bytes();
+  out[4] = c->pst[0].bytes() + c->pst[1].bytes();
+  out[5] = c->sigs.cap + c->pks.cap + c->msgs.cap + c->off.cap + c->acc.cap + c->fblob.cap;
+  out[6] = c->comb ? uint64_t(kCombRows) * kCombEntries * kBStride * 4 : 0;
+  for (int k = 1; k < 7; k++) out[0] += out[k];
+  return 0;
+}
+
 int edv_pick_device(uint32_t device_mask) {
   g_err.clear();
   int err;
@@ -1313,7 +1456,8 @@ int edv_wait_async(int device, int64_t ticket) {
       if (s.ticket == ticket) async_fail(*cl.c, s);
       return set_err(EDV_E_HIP, "async wait", e);
     }
-    return s.ticket == ticket ? async_complete(*cl.c, s) : 0;
+    if (s.ticket == ticket) return async_complete(*cl.c, s);
+    break;  // a submission reusing the slot completed it meanwhile: its outcome is in the ledger
   }
   // already complete (waited for, or its slot was reused) -- unless a batch at
   // or after it failed (sticky, edv_ledger.h)
@@ -1409,27 +1553,6 @@ int edv_pipeline_sync(int device) {
   return 0;
 }
 
-int edv_time_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
-                       const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, int device,
-                       int iters, float* ms_out) {
-  g_err.clear();
-  int err;
-  if ((err = check_dev_align(d_sigs, d_pks, d_msg_off))) return err;
-  CtxLock cl(device);
-  if (cl.err) return cl.err;
-  DevCtx* c = cl.c;
-  Events ev;
-  if ((err = ev.create(2))) return err;
-  HIPOK(hipEventRecord(ev.e[0], c->stream), "record");
-  for (int it = 0; it < iters; it++)
-    if ((err = launch(*c, d_sigs, d_pks, d_msgs, d_msg_off, msg_base, n, d_accept, c->stream, 0))) return err;
-  HIPOK(hipEventRecord(ev.e[1], c->stream), "record");
-  HIPOK(hipEventSynchronize(ev.e[1]), "event sync");
-  float ms = 0;
-  HIPOK(hipEventElapsedTime(&ms, ev.e[0], ev.e[1]), "elapsed");
-  if (ms_out) *ms_out = ms;
-  return 0;
-}
 
 static int ensure_comb(DevCtx& c) {
   if (c.comb) return 0;
@@ -1491,9 +1614,7 @@ int edv_set_chunk(int device, uint64_t chunk) {
   if (chunk < kBlock || chunk > (uint64_t(1) << 24)) return set_err(EDV_E_ARG, "chunk out of range");
   int err;
   if ((err = drain(*c))) return err;  // nothing may still use the scratch being reallocated
-  c->chunk = (chunk / kBlock) * kBlock;
-  if (c->st.ensure(c->chunk)) return EDV_E_OOM;
-  if (c->pipe_ready && (c->pst[0].ensure(c->chunk) || c->pst[1].ensure(c->chunk))) return EDV_E_OOM;
+  c->chunk = (chunk / kBlock) * kBlock;  // the scratch grows to it by use
   return 0;
 }
 
@@ -1519,72 +1640,7 @@ int edv_set_length_buckets(int device, int mode) {
   return 0;
 }
 
-int edv_profile_batch_dev_flush(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
-                                const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept,
-                                int device, int iters, uint64_t flush_bytes, float* ms_prep, float* ms_flush,
-                                float* ms_main) {
-  g_err.clear();
-  int err;
-  if ((err = check_dev_align(d_sigs, d_pks, d_msg_off))) return err;
-  CtxLock cl(device);
-  if (cl.err) return cl.err;
-  DevCtx* c = cl.c;
-  if (n == 0 || n > c->chunk || iters <= 0) return set_err(EDV_E_ARG, "profile needs 0 < n <= chunk, iters > 0");
-  const bool bucket = bucketing_enabled(*c, 0);
-  VerifyArgs va = make_args(*c, c->st, d_sigs, d_pks, d_msgs, d_msg_off, msg_base, d_accept, bucket);
-  va.n = n;
-  uint32_t* hist = bucket_ctr(c->st, 0);
-  const unsigned blocks = unsigned((n + kBlock - 1) / kBlock);
-  // the flush buffer lives for this call only (DevBuf keeps its memory; this frees it)
-  struct FlushBuf : DevBuf {
-    ~FlushBuf() {
-      if (p) (void)hipFree(p);
-    }
-  } flush;
-  flush_bytes &= ~uint64_t(15);
-  if (flush_bytes && flush.ensure(flush_bytes)) return EDV_E_OOM;
-  if (flush_bytes) HIPOK(hipMemsetAsync(flush.p, 0, flush_bytes, c->stream), "memset flush");
-  Events ev;
-  if ((err = ev.create(4))) return err;
-  HIPOK(hipStreamWaitEvent(c->stream, c->st_done, 0), "wait scratch");
-  float tp = 0, tf = 0, tm = 0;
-  for (int it = 0; it < iters; it++) {
-    if (bucket) {
-      HIPOK(hipMemsetAsync(hist, 0, 2 * kBuckets * 4, c->stream), "memset buckets");
-      HIPOK(launch_bucket_kernels(blocks, c->stream, d_msg_off, 0, n, hist, const_cast<uint32_t*>(va.st.perm)),
-            "bucket launch");
-    }
-    HIPOK(hipEventRecord(ev.e[0], c->stream), "record");
-    HIPOK(launch_prep_kernel(3 * blocks, c->stream, va), "prep launch");
-    HIPOK(hipEventRecord(ev.e[1], c->stream), "record");
-    if (flush_bytes)
-      HIPOK(launch_flush_kernel(c->stream, flush.p, flush_bytes), "flush launch");
-    HIPOK(hipEventRecord(ev.e[2], c->stream), "record");
-    HIPOK(launch_main_kernel(blocks, c->stream, va, false), "main launch");
-    HIPOK(hipEventRecord(ev.e[3], c->stream), "record");
-    HIPOK(hipEventSynchronize(ev.e[3]), "event sync");
-    float a = 0, b = 0, m = 0;
-    HIPOK(hipEventElapsedTime(&a, ev.e[0], ev.e[1]), "elapsed");
-    HIPOK(hipEventElapsedTime(&b, ev.e[1], ev.e[2]), "elapsed");
-    HIPOK(hipEventElapsedTime(&m, ev.e[2], ev.e[3]), "elapsed");
-    tp += a;
-    tf += b;
-    tm += m;
-  }
-  HIPOK(hipEventRecord(c->st_done, c->stream), "record scratch");
-  HIPOK(hipStreamSynchronize(c->stream), "stream sync");  // the flush buffer is freed on return
-  if (ms_prep) *ms_prep = tp / iters;
-  if (ms_flush) *ms_flush = tf / iters;
-  if (ms_main) *ms_main = tm / iters;
-  return 0;
-}
 
-int edv_profile_batch_dev(const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
-                          const uint64_t* d_msg_off, uint64_t msg_base, uint64_t n, uint8_t* d_accept, int device,
-                          int iters, float* ms_prep, float* ms_main) {
-  return edv_profile_batch_dev_flush(d_sigs, d_pks, d_msgs, d_msg_off, msg_base, n, d_accept, device, iters, 0,
-                                     ms_prep, nullptr, ms_main);
-}
 
 int edv_dev_alloc(int device, uint64_t bytes, void** out) {
   int phys, err;
@@ -1638,3 +1694,7 @@ int edv_host_free(void* p) {
 }
 
 }  // extern "C"
+
+#ifdef EDV_MEASUREMENT_API
+#include "edv_measure.inc"
+#endif

@@ -238,26 +238,16 @@ __global__ __launch_bounds__(kBlock) void edv_pack_bits_kernel(const uint8_t* ac
   bits[k] = uint8_t(b);
 }
 
-// Measurement helper of edv_profile_batch_dev_flush: read and rewrite a buffer
-// larger than the Infinity Cache, so whatever the previous kernel left there
-// (the prep kernel's tables) is evicted before the next one runs.
-__global__ __launch_bounds__(kBlock) void edv_flush_kernel(int4* p, uint64_t n16) {
-  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * kBlock) {
-    int4 v = p[i];
-    v.x += 1;
-    p[i] = v;
-  }
+// An [S]B table set, once per GPU: the base points 2^(bits t) B first (one
+// lane each), then j x base t for t = 0..tables-1, j = 0..2^(bits-1), affine
+// precomp form, one entry per lane.
+__global__ void edv_bbase_kernel(ge_p3* bases, SbShape sh) {
+  if (int(threadIdx.x) < sh.tables) bases[threadIdx.x] = base_point(int(threadIdx.x) * sh.bits);
 }
-
-// The [S]B tables, once per device: the base points 2^(kBBits t) B first
-// (one lane each), then j x base t for t = 0..kBTables-1, j = 0..2^(kBBits-1),
-// affine precomp form, one entry per lane.
-__global__ void edv_bbase_kernel(ge_p3* bases) {
-  if (threadIdx.x < kBTables) bases[threadIdx.x] = base_point(int(threadIdx.x) * kBBits);
-}
-__global__ void edv_btab_kernel(int32_t* out, const ge_p3* bases) {
+__global__ void edv_btab_kernel(int32_t* out, const ge_p3* bases, SbShape sh) {
   const uint32_t t = threadIdx.x + blockIdx.x * blockDim.x;
-  if (t < uint32_t(kBTables * kBEntries)) btab_entry(out + size_t(t) * kBStride, int(t % kBEntries), bases[t / kBEntries]);
+  if (t < uint32_t(sh.tables * sh.entries))
+    btab_entry(out + size_t(t) * kBStride, int(t % uint32_t(sh.entries)), bases[t / uint32_t(sh.entries)]);
 }
 
 // Row f-3: SHA-256 of n messages, one per lane -> 32-byte digests (out: n x 8 words).
@@ -289,10 +279,10 @@ hipError_t launch_bucket_kernels(unsigned blocks, hipStream_t s, const uint64_t*
   edv_bucket_scatter_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(off, base, n, ctr, ctr + kBuckets, perm);
   return hipGetLastError();
 }
-hipError_t launch_btab_kernel(hipStream_t s, int32_t* out) {
-  ge_p3* bases = reinterpret_cast<ge_p3*>(out + kBTabWords);
-  edv_bbase_kernel<<<1, 64, 0, s>>>(bases);
-  edv_btab_kernel<<<(kBTables * kBEntries + 63) / 64, 64, 0, s>>>(out, bases);
+hipError_t launch_btab_kernel(hipStream_t s, int32_t* out, SbShape sh) {
+  ge_p3* bases = reinterpret_cast<ge_p3*>(out + sb_words(sh));
+  edv_bbase_kernel<<<1, 64, 0, s>>>(bases, sh);
+  edv_btab_kernel<<<(sh.tables * sh.entries + 63) / 64, 64, 0, s>>>(out, bases, sh);
   return hipGetLastError();
 }
 hipError_t launch_comb_kernel(hipStream_t s, int32_t* out) {
@@ -313,10 +303,6 @@ hipError_t launch_pack_bits_kernel(hipStream_t s, const uint8_t* acc, uint64_t n
 hipError_t launch_sha256_kernel(unsigned blocks, hipStream_t s, const uint8_t* msgs, const uint64_t* off,
                                 uint64_t msg_base, uint64_t n, uint32_t* out) {
   edv_sha256_kernel<<<dim3(blocks), dim3(kBlock), 0, s>>>(msgs, off, msg_base, n, out);
-  return hipGetLastError();
-}
-hipError_t launch_flush_kernel(hipStream_t s, void* p, uint64_t bytes) {
-  edv_flush_kernel<<<dim3(4096), dim3(kBlock), 0, s>>>(static_cast<int4*>(p), bytes / 16);
   return hipGetLastError();
 }
 

@@ -37,17 +37,30 @@ namespace edv {
 constexpr int kAWin = 4;                        // bits per [a](-A) / [b](SB - R) window
 constexpr int kAWindows = (255 + kAWin - 1) / kAWin;  // at most: 64 x 4 = 256 bits >= 253
 constexpr int kAEntries = (1 << (kAWin - 1)) + 1;     // per-lane table 0..8 x P, cached form (entry 0 = identity)
-// [S]B (prep kernel, R side): 12 signed radix-2^22 digits of S against shared
-// tables t = 0..11 of 0..2^21 x 2^(22 t) B (affine precomp form, 256 MiB each,
-// 3 GiB per device: memory the 288 GB of HBM has to spare buys mixed additions --
-// radix 2^16 (16 additions, 64 MiB) made the C2 step 1.1 % slower, 2^19 (14)
-// 0.8 %, profiles/r05/ab_bbits_s13.jsonl; the gathers are staged ahead, so the
-// tables' size costs no latency)
-constexpr int kBBits = 22;
+// [S]B (prep kernel, R side): signed radix-2^bits digits of S against shared
+// tables t of 0..2^(bits-1) x 2^(bits t) B (affine precomp form).  Two shapes,
+// chosen per launch (SbShape below): the LARGE one, 12
+// digits of 22 bits against 3 GiB of tables (256 MiB each), built in a device
+// context once a batch of at least one wave per SIMD arrives (memory the 288 GB
+// of HBM has to spare buys mixed additions: radix 2^16 made the C2 step 1.1 %
+// slower, 2^19 0.8 %, profiles/r05/ab_bbits_s13.jsonl; the gathers are staged
+// ahead, so the tables' size costs no latency), and the COMPACT one, 16 digits
+// of 16 bits against 64 MiB, which every context builds first and which is all
+// a Node verifying prods of a few hundred requests ever allocates.
+constexpr int kBBits = 22;                             // the large shape
 constexpr int kBTables = (253 + kBBits - 1) / kBBits;  // 12: digit t of S against table t
 constexpr int kBEntries = (1 << (kBBits - 1)) + 1;     // per table 0..2^(kBBits-1) x base
-// the top digit, (S >> kBBits (kBTables - 1)) + carry, must index its table too
+constexpr int kBBitsCompact = 16;
+constexpr int kBTablesCompact = (253 + kBBitsCompact - 1) / kBBitsCompact;  // 16
+constexpr int kBEntriesCompact = (1 << (kBBitsCompact - 1)) + 1;
+// the top digit, (S >> bits (tables - 1)) + carry, must index its table too
 static_assert(253 - kBBits * (kBTables - 1) <= kBBits - 1, "top [S]B digit out of table range");
+static_assert(253 - kBBitsCompact * (kBTablesCompact - 1) <= kBBitsCompact - 1, "top [S]B digit out of table range");
+struct SbShape {
+  int bits, tables, entries;
+};
+EDV_HD constexpr SbShape sb_large() { return SbShape{kBBits, kBTables, kBEntries}; }
+EDV_HD constexpr SbShape sb_compact() { return SbShape{kBBitsCompact, kBTablesCompact, kBEntriesCompact}; }
 constexpr int kCombEntries = 129;               // signer comb rows: 0..128 x 256^i B
 constexpr int kBStride = 32;                    // words per B / comb entry (30 used; 128-byte aligned)
 
@@ -562,7 +575,7 @@ EDV_HD ge_p3 base_point(int shift) {
   for (int k = 0; k < shift; k++) B = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(B)));
   return B;
 }
-// j * base for j in [0, 2^(kBBits-1)], affine precomp form, written as kBStride words.
+// j * base for j in [0, 2^(kBBits-1)] (j < 2^kBBits), affine precomp form, written as kBStride words.
 EDV_HD void btab_entry(int32_t* o, int j, const ge_p3& base) {
   const ge_cached Bc = ge_p3_to_cached(base);
   ge_p3 acc = ge_p3_identity();
@@ -578,6 +591,11 @@ EDV_HD void btab_entry(int32_t* o, int j, const ge_p3& base) {
   o[30] = 0;
   o[31] = 0;
 }
+
+// Device words of a table set: tables x entries x kBStride, then the tables'
+// base points 2^(bits t) B as scratch for the build (launch_btab_kernel).
+EDV_HD constexpr size_t sb_words(SbShape sh) { return size_t(sh.tables) * size_t(sh.entries) * kBStride; }
+EDV_HD constexpr size_t sb_alloc_bytes(SbShape sh) { return 4 * sb_words(sh) + size_t(sh.tables) * sizeof(ge_p3); }
 
 // Per-lane outputs of phase 1 that phase 2 consumes.
 struct PrepDigits {
@@ -665,43 +683,57 @@ EDV_HD bool prep_point(const uint32_t P[8], ATab& tab) {
 // is canonical and a curve point's encoding, so R bytes that are
 // non-canonical, of small order (libsodium's blocklist) or decode to no point
 // can never pass: the same three checks as for A reject them.  [S]B is the
-// sum of entry |d_t| of table t (negated for d_t < 0) over the kBTables signed
-// radix-2^kBBits digits d_t of S, added to -R by mixed additions; BTab provides
-// stage(t, j) then fetch() -> j x 2^(kBBits t) B (precomp).  S < L for every signature that can
+// sum of entry |d_t| of table t (negated for d_t < 0) over the sh.tables signed
+// radix-2^sh.bits digits d_t of S (sh = bt.shape(): the large or the compact
+// tables), added to -R by mixed additions; BTab provides stage(t, j) then
+// fetch() -> j x 2^(bits t) B (precomp).  S < L for every signature that can
 // pass (the hash side's V2 check rejects the rest); S is cut to 253 bits so
 // that any 256-bit S keeps its digits inside the tables.  BTab also stashes
 // Q's cached form for the table (build_table_projective).
-template <class ATab, class BTab>
-EDV_HD bool prep_rpoint(const uint32_t R[8], const uint32_t S[8], ATab& tab, BTab& bt) {
+EDV_HD void shr256_var(uint32_t v[8], int n) {  // 0 < n < 32
+#pragma unroll
+  for (int i = 0; i < 7; i++) v[i] = (v[i] >> n) | (v[i + 1] << (32 - n));
+  v[7] >>= n;
+}
+// Q = [S]B - R (projective) for a decodable R; false if R is rejected
+template <class BTab>
+EDV_HD bool rpoint_q(const uint32_t R[8], const uint32_t S[8], BTab& bt, ge_p3& q) {
   if (!ge_is_canonical(R) || has_small_order(R)) return false;
-  ge_p3 q;
   if (!ge_frombytes_negate(q, R)) return false;
+  const SbShape sh = bt.shape();
   uint32_t s[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) s[i] = S[i];
   s[7] &= 0x1fffffffu;
   // signed digits, least significant first, taken off the bottom of s as the
-  // walk goes: d = (s mod 2^kBBits) + carry in [-2^(kBBits-1), 2^(kBBits-1));
-  // the top digit keeps its carry (static_assert above: it stays in range)
+  // walk goes: d = (s mod 2^bits) + carry in [-2^(bits-1), 2^(bits-1)); the
+  // top digit keeps its carry (static_asserts above: it stays in range)
   int carry = 0;
+  const int bits = sh.bits;
   auto next_digit = [&](bool top) {
-    int e = int(s[0] & ((1u << kBBits) - 1)) + carry;
-    shr256<kBBits>(s);
-    carry = top ? 0 : (e + (1 << (kBBits - 1))) >> kBBits;
-    return e - carry * (1 << kBBits);
+    int e = int(s[0] & ((1u << bits) - 1)) + carry;
+    shr256_var(s, bits);
+    carry = top ? 0 : (e + (1 << (bits - 1))) >> bits;
+    return e - carry * (1 << bits);
   };
   // entry t + 1 is staged (on the GPU: straight into LDS) while entry t is added
-  int dt = next_digit(kBTables == 1);
+  int dt = next_digit(sh.tables == 1);
   bt.stage(0, dt < 0 ? -dt : dt);
 #pragma unroll 1
-  for (int t = 0; t < kBTables; t++) {
+  for (int t = 0; t < sh.tables; t++) {
     const ge_precomp e = ge_precomp_cneg(bt.fetch(), dt < 0);
-    if (t + 1 < kBTables) {
-      dt = next_digit(t + 2 == kBTables);
+    if (t + 1 < sh.tables) {
+      dt = next_digit(t + 2 == sh.tables);
       bt.stage(t + 1, dt < 0 ? -dt : dt);
     }
     q = ge_p1p1_to_p3(ge_madd(q, e));
   }
+  return true;
+}
+template <class ATab, class BTab>
+EDV_HD bool prep_rpoint(const uint32_t R[8], const uint32_t S[8], ATab& tab, BTab& bt) {
+  ge_p3 q;
+  if (!rpoint_q(R, S, bt, q)) return false;
   build_table_projective(tab, q, bt);
   return true;
 }

@@ -22,6 +22,10 @@ from . import _edvhost  # native host-side packing (csrc/edv_host.cpp, row f-1)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("EDV_LIB", os.path.join(_HERE, "libedv.so"))
+# the benchmark/profiling build (include/edv_measure.h): loaded only by the
+# measurement helpers below (bench.py, tools/, the GPU tests' fault hook),
+# never by the authenticators
+MEASURE_LIB_PATH = os.path.join(_HERE, "libedv_measure.so")
 MEASUREMENT_TAG = "MEASUREMENT-ONLY"  # in edv_version() of builds whose verdicts are not libsodium's
 
 EDV_OK = 0
@@ -92,18 +96,8 @@ def lib():
         h.edv_wait_async.restype = ctypes.c_int
         h.edv_pipeline_sync.argtypes = [ctypes.c_int]
         h.edv_pipeline_sync.restype = ctypes.c_int
-        h.edv_time_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int,
-                                         ctypes.POINTER(ctypes.c_float)]
-        h.edv_time_batch_dev.restype = ctypes.c_int
         h.edv_sign_batch_dev.argtypes = [vp, vp, vp, u64, u64, vp, vp, ctypes.c_int, vp]
         h.edv_sign_batch_dev.restype = ctypes.c_int
-        h.edv_profile_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int,
-                                            ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
-        h.edv_profile_batch_dev.restype = ctypes.c_int
-        h.edv_profile_batch_dev_flush.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int, u64,
-                                                  ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
-                                                  ctypes.POINTER(ctypes.c_float)]
-        h.edv_profile_batch_dev_flush.restype = ctypes.c_int
         h.edv_stream.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         h.edv_stream.restype = ctypes.c_int
         h.edv_sync.argtypes = [ctypes.c_int]
@@ -128,6 +122,8 @@ def lib():
         h.edv_pick_device.restype = ctypes.c_int
         h.edv_pack_bits_dev.argtypes = [vp, u64, vp, ctypes.c_int, vp]
         h.edv_pack_bits_dev.restype = ctypes.c_int
+        h.edv_context_memory.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+        h.edv_context_memory.restype = ctypes.c_int
         h.edv_dev_alloc.argtypes = [ctypes.c_int, u64, ctypes.POINTER(ctypes.c_void_p)]
         h.edv_dev_free.argtypes = [ctypes.c_int, vp]
         h.edv_h2d.argtypes = [ctypes.c_int, vp, vp, u64]
@@ -138,8 +134,61 @@ def lib():
         return h
 
 
+_mlib = None
+
+
+def measure_lib():
+    """libedv_measure.so: the same verifier plus kernel timing and the fault hook
+    (include/edv_measure.h).  Its device contexts are its own (a second [S]B
+    table set and scratch per GPU in this process); device pointers from either
+    library may be passed to the other."""
+    global _mlib
+    if _mlib is not None:
+        return _mlib
+    with _lock:
+        if _mlib is not None:
+            return _mlib
+        if not os.path.exists(MEASURE_LIB_PATH):
+            raise EdvUnavailable("libedv_measure.so not built at {} (run __graft_entry__.build())"
+                                 .format(MEASURE_LIB_PATH))
+        h = ctypes.CDLL(MEASURE_LIB_PATH)
+        vp, u64, f32p = ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_float)
+        h.edv_time_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int, f32p]
+        h.edv_profile_batch_dev.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int, f32p, f32p]
+        h.edv_profile_batch_dev_flush.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int, u64,
+                                                  f32p, f32p, f32p]
+        h.edv_profile_prep_sides.argtypes = [vp, vp, vp, vp, u64, u64, vp, ctypes.c_int, ctypes.c_int, f32p]
+        h.edv_test_fail_async.argtypes = [ctypes.c_int, ctypes.c_int64]
+        h.edv_verify_batch_async.argtypes = [vp, vp, vp, vp, u64, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+        h.edv_wait_async.argtypes = [ctypes.c_int, ctypes.c_int64]
+        h.edv_last_error.restype = ctypes.c_char_p
+        h.edv_version.restype = ctypes.c_char_p
+        _mlib = h
+        return h
+
+
+def _mcheck(rc):
+    if rc != EDV_OK:
+        what = measure_lib().edv_last_error().decode(errors="replace")
+        if rc == EDV_E_NODEV:
+            raise EdvUnavailable(what)
+        raise EdvError(rc, what)
+
+
 def version() -> str:
     return lib().edv_version().decode()
+
+
+CONTEXT_MEMORY_FIELDS = ("total", "sb_tables", "chunk_scratch", "async_slots", "pipelined_sets", "sync_inputs",
+                         "signer_comb")
+
+
+def context_memory(device: int = 0) -> dict:
+    """Device bytes the library holds for `device` in this process
+    (edv_context_memory), by kind; all zero before the context exists."""
+    out = (ctypes.c_uint64 * 7)()
+    _check(lib().edv_context_memory(device, out))
+    return dict(zip(CONTEXT_MEMORY_FIELDS, (int(x) for x in out)))
 
 
 def device_count() -> int:
@@ -500,26 +549,39 @@ def sign_arrays(seeds, msgs, offsets, device=0):
     return dp.download(32 * n), ds.download(64 * n)
 
 
+# ---- measurement helpers: libedv_measure.so (include/edv_measure.h)
 def time_device(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, iters=1, msg_base=0) -> float:
     """Milliseconds for `iters` back-to-back kernel launches (HIP events on the kernel's stream)."""
     ms = ctypes.c_float(0)
-    _check(lib().edv_time_batch_dev(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, iters,
-                                    ctypes.byref(ms)))
+    _mcheck(measure_lib().edv_time_batch_dev(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, iters,
+                                             ctypes.byref(ms)))
     return float(ms.value)
 
 
 def profile_device(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, iters=1, msg_base=0):
     """(prep_ms, main_ms): average per-launch kernel times from HIP events on the kernels' stream."""
     a, b = ctypes.c_float(0), ctypes.c_float(0)
-    _check(lib().edv_profile_batch_dev(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, iters,
-                                       ctypes.byref(a), ctypes.byref(b)))
+    _mcheck(measure_lib().edv_profile_batch_dev(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, iters,
+                                                ctypes.byref(a), ctypes.byref(b)))
     return float(a.value), float(b.value)
 
 
 def profile_device_flush(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, iters=1, flush_bytes=0, msg_base=0):
     """(prep_ms, flush_ms, main_ms) with a cache-evicting kernel of flush_bytes between
-    prep and main (edv_profile_batch_dev_flush; measurement only)."""
+    prep and main (edv_profile_batch_dev_flush)."""
     a, f, b = ctypes.c_float(0), ctypes.c_float(0), ctypes.c_float(0)
-    _check(lib().edv_profile_batch_dev_flush(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, iters,
-                                             flush_bytes, ctypes.byref(a), ctypes.byref(f), ctypes.byref(b)))
+    _mcheck(measure_lib().edv_profile_batch_dev_flush(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device,
+                                                      iters, flush_bytes, ctypes.byref(a), ctypes.byref(f),
+                                                      ctypes.byref(b)))
     return float(a.value), float(f.value), float(b.value)
+
+
+PREP_SIDE_KEYS = ("hash_side", "a_side", "r_side", "all_three", "point_sides")
+
+
+def profile_prep_sides(d_sigs, d_pks, d_msgs, d_off, n, d_accept, device=0, iters=1, msg_base=0) -> dict:
+    """The prep kernel's sides timed apart (edv_profile_prep_sides), ms per launch."""
+    ms = (ctypes.c_float * 5)()
+    _mcheck(measure_lib().edv_profile_prep_sides(d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, device, iters,
+                                                 ms))
+    return dict(zip(PREP_SIDE_KEYS, (float(x) for x in ms)))

@@ -258,6 +258,18 @@ class DeviceBatch:
         edv.pack_bits_device(self.d_accept.ptr, self.n, self._bits.ptr, self.device)
         return self._bits.download(nb)
 
+    def host_prefix(self, k):
+        """(sigs, pks, msgs, off, expected) host arrays of the first k requests,
+        read back from the device (the message bytes included, so it works for
+        batches built with keep_host=False); offsets rebased to 0."""
+        k = min(k, self.n)
+        off = self.host_off[:k + 1] - self.host_off[0]
+        mb = int(off[-1])
+        msgs = np.zeros(mb + 64, np.uint8)
+        msgs[:mb] = self.d_msgs.download_at(int(self.host_off[0]), mb)
+        return (self.d_sigs.download_at(0, 64 * k), self.d_pks.download_at(0, 32 * k), msgs,
+                np.ascontiguousarray(off), self.expected()[:k])
+
     def host_copy(self):
         """(sigs, pks, msgs, off) host arrays of this batch."""
         if self.host_msgs is None:

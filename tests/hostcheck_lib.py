@@ -29,6 +29,9 @@ def _bind(lib):
     lib.hc_recode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p]
     lib.hc_btab_entries_of.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     lib.hc_rside_point.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p]
+    lib.hc_btab_entries_of_bits.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_void_p]
+    lib.hc_rside_point_bits.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p]
     lib.hc_half_scalars.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.hc_verify_batch.argtypes = [ctypes.c_char_p] * 3 + [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
     lib.hc_layout.argtypes = [ctypes.c_void_p]

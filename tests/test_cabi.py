@@ -1,6 +1,7 @@
 """The product C-ABI library builds, loads without a GPU and exports every
-symbol include/edv.h declares; without a GPU the shim fails loudly (no CPU
-fallback)."""
+symbol include/edv.h declares and nothing of the measurement header
+include/edv_measure.h (that is libedv_measure.so's); without a GPU the shim
+fails loudly (no CPU fallback)."""
 import ctypes
 import os
 import re
@@ -11,29 +12,46 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR = os.path.join(ROOT, "include", "edv.h")
+MHDR = os.path.join(ROOT, "include", "edv_measure.h")
 
 
-def declared():
-    src = open(HDR).read()
+def declared(hdr=HDR):
+    src = open(hdr).read()
     return sorted(set(re.findall(r"^\s*(?:int|const char \*|void)\s*\**\s*(edv_\w+)\s*\(", src, re.M)))
+
+
+def exported(path):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", path]).decode()
+    return set(re.findall(r" T (edv_\w+)$", out, re.M))
 
 
 def test_header_declares_the_core_entry_points():
     names = declared()
     for need in ("edv_verify_batch", "edv_verify_batch_dev", "edv_version", "edv_last_error", "edv_device_count",
-                 "edv_sign_batch_dev", "edv_profile_batch_dev", "edv_time_batch_dev", "edv_set_chunk"):
+                 "edv_sign_batch_dev", "edv_set_chunk", "edv_context_memory", "edv_verify_batch_async"):
         assert need in names
+    meas = declared(MHDR)
+    for need in ("edv_profile_batch_dev", "edv_profile_batch_dev_flush", "edv_time_batch_dev",
+                 "edv_profile_prep_sides", "edv_test_fail_async"):
+        assert need in meas and need not in names
 
 
 def test_library_exports_every_declared_symbol():
+    """the product library exports exactly the product
+    header's entry points -- no kernel timing, cache flush or fault hook -- and
+    the measurement build exports both headers'."""
     from indy_plenum_amd import edv
     lib = edv.lib()
     missing = [n for n in declared() if not hasattr(lib, n)]
     assert missing == []
-    out = subprocess.check_output(["nm", "-D", "--defined-only", edv.LIB_PATH]).decode()
-    exported = set(re.findall(r" T (edv_\w+)$", out, re.M))
-    assert set(declared()) <= exported
+    prod = exported(edv.LIB_PATH)
+    assert prod == set(declared())
+    assert not (prod & set(declared(MHDR)))
+    meas = exported(edv.MEASURE_LIB_PATH)
+    assert meas == set(declared()) | set(declared(MHDR))
     assert edv.version().startswith("edv ") and "gfx950" in edv.version()
+    blob = open(edv.LIB_PATH, "rb").read()
+    assert b"edv_flush_kernel" not in blob and b"edv_flush_kernel" in open(edv.MEASURE_LIB_PATH, "rb").read()
 
 
 def test_library_contains_gfx950_code_object():

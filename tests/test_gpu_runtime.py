@@ -632,6 +632,7 @@ def test_bench_default_line_contract():
     assert (rf["traffic"] is not None) == pmc_matches
     cb = line["cpu_baseline"]
     assert cb["kind"] in ("reference", "port") and cb["value"] > 0 and cb["cores"] >= 1 and cb["sample"]
+    assert 0 < rf["job_frac"] <= 1 and rf["rank0_kernel_frac"] == rf["frac"]
 
 
 def test_bench_c3_mode_bounded():
@@ -705,8 +706,8 @@ def test_bench_c3_full_size_virtual_ranks(ranks):
     construction (5 % damaged at known positions)."""
     env = dict(os.environ, EDV_VIRTUAL_DEVICES=str(ranks))
     env.pop("WORLD_SIZE", None)
-    line = _bench(["--gpus", str(ranks), "--steps", "2", "--reps", "1", "--warmup", "1", "--warmup-seconds", "0"],
-                  env=env, timeout=900)
+    line = _bench(["--gpus", str(ranks), "--steps", "2", "--reps", "1", "--warmup", "1", "--warmup-seconds", "0",
+                   "--cpu-seconds", "3"], env=env, timeout=900)
     assert line["n_gpus"] == ranks and line["verdicts_as_expected"] is True
     assert line["config"]["total_per_step"] == 16777216 and line["config"]["per_gpu"] == 16777216 // ranks
     mg = line["multi_gpu"]
@@ -715,3 +716,102 @@ def test_bench_c3_full_size_virtual_ranks(ranks):
     assert mg["one_gpu_same_workload_verifies_per_s"] > 1e6
     assert "scaling_efficiency" not in mg
     assert line["value"] > 1e7
+    # north_star's reporting clause at N > 1 -- the whole
+    # job's fraction of N GPUs' INT32 peak beside rank 0's kernel
+    # fraction, and libsodium on the host cores in the same run, cores stated
+    rf = line["roofline"]
+    assert 0 < rf["job_frac"] <= 1 and 0 < rf["rank0_kernel_frac"] <= 1
+    from bench import w_total, PEAK_INT32
+    assert abs(rf["job_frac"] - line["value"] * w_total(256) / (ranks * PEAK_INT32)) < 1e-9
+    cb = line["cpu_baseline"]
+    assert cb["kind"] == "reference" and cb["value"] > 0 and cb["cores"] >= 1
+    assert "C3 shard" in cb["sample"] and line["gpu_over_cpu"] > 1
+
+
+def test_async_failure_end_to_end_with_fault_hook():
+    """the asynchronous path's fail-closed contract driven on the
+    device, not only the ledger's arithmetic.  libedv_measure.so's fault hook
+    (edv_test_fail_async) makes one submission launch nothing and fail at its
+    wait, as a batch whose done event failed would.  Then: the failed ticket's
+    wait returns EDV_E_HIP and its verdicts (zeroed at submission) are all
+    rejections; a ticket waited for before the failure and asked again is
+    reported failed (sticky); batches submitted around it, still in their
+    slots, keep their own verdicts; later batches (every slot reused) are
+    unaffected -- with pageable and with page-locked (zero-copy) verdicts."""
+    import ctypes
+    ml = edv.measure_lib()
+    dev = 0
+    n = 512
+    sigs, pks, msgs, off = orc.corpus(0xFA17, 0, n, mode=1, invalid_permille=100)
+    want = checker(sigs, pks, msgs, off)
+    assert 0 < want.sum() < n
+    pin = edv.PinnedBuffer(n * 16)
+
+    def submit(acc):
+        t = ctypes.c_int64(-1)
+        rc = ml.edv_verify_batch_async(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, off.ctypes.data, n,
+                                       acc.ctypes.data, dev, ctypes.byref(t))
+        assert rc == 0, ml.edv_last_error()
+        return t.value
+
+    def wait(t):
+        return ml.edv_wait_async(dev, t)
+
+    for pinned in (False, True):
+        accs = ([pin.array[k * n:(k + 1) * n] for k in range(16)] if pinned
+                else [np.full(n, 7, np.uint8) for _ in range(16)])
+        t0 = submit(accs[0])
+        assert wait(t0) == 0 and np.array_equal(accs[0], want)
+        t1 = submit(accs[1])
+        assert ml.edv_test_fail_async(dev, t1 + 1) == 0
+        t2 = submit(accs[2])
+        t3 = submit(accs[3])
+        assert (t1, t2, t3) == (t0 + 1, t0 + 2, t0 + 3)
+        assert wait(t3) == 0 and np.array_equal(accs[3], want)
+        assert wait(t2) == edv.EDV_E_HIP
+        assert not accs[2].any()                  # zeroed at submission, nothing written after
+        assert wait(t1) == 0 and np.array_equal(accs[1], want)   # still in its slot: its own verdicts
+        assert wait(t0) == edv.EDV_E_HIP          # settled below the failed ticket: sticky
+        assert wait(t2) == edv.EDV_E_HIP          # and the failed one stays failed
+        assert ml.edv_test_fail_async(dev, -1) == 0
+        later = [submit(accs[4 + k]) for k in range(10)]   # every slot reused after the failure
+        for k, t in enumerate(later):
+            assert wait(t) == 0 and np.array_equal(accs[4 + k], want), (pinned, k)
+        assert wait(later[-1] + 1) == edv.EDV_E_ARG  # never issued
+    pin.free()
+
+
+def test_context_memory_and_table_sets():
+    """edv_context_memory reports the library's device
+    memory by kind.  In a fresh process with the default table policy a
+    Node-sized batch builds only the compact [S]B set (64 MiB) and scratch
+    sized to the batch, well under 1.5 GB; a C2-sized batch then adds the
+    large set (3 GiB); EDV_SB_TABLES=compact never builds it.  Verdicts equal
+    libsodium's in every configuration."""
+    code = r'''
+import json, sys, numpy as np
+sys.path.insert(0, %r); sys.path.insert(0, %r)
+import oracle_lib as orc
+from indy_plenum_amd import edv
+out = {}
+for n in (400, 65536):
+    s, p, m, o = orc.corpus(0xF00D, 0, n, mode=0, invalid_permille=50)
+    acc = edv.verify_arrays(s, p, m, o)
+    want = orc.sodium_verify_batch(s, p, m, o, 16) if orc.sodium_batch() else acc
+    out[str(n)] = {"equal": bool(np.array_equal(acc, want)), "mem": edv.context_memory(0)}
+print(json.dumps(out))
+''' % (ROOT, os.path.join(ROOT, "tests"))
+    res = {}
+    for pol in ("auto", "compact"):
+        env = dict(os.environ, EDV_SB_TABLES=pol)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[pol] = json.loads(r.stdout.strip().splitlines()[-1])
+    for pol, d in res.items():
+        assert d["400"]["equal"] and d["65536"]["equal"], pol
+        m = d["400"]["mem"]
+        assert m["sb_tables"] < 80 * 2**20, (pol, m)             # compact set only
+        assert 0 < m["total"] < 1.5 * 2**30, (pol, m)
+        assert m["total"] == sum(v for k, v in m.items() if k != "total")
+    assert res["auto"]["65536"]["mem"]["sb_tables"] > 3 * 2**30    # large set added at C2 size
+    assert res["compact"]["65536"]["mem"]["sb_tables"] < 80 * 2**20

@@ -5,6 +5,8 @@ import ctypes
 import hashlib
 import random
 
+import pytest
+
 import golden_io
 import hostcheck_lib
 
@@ -236,29 +238,37 @@ def test_walk_layout_constants():
     assert lay["bbits"] * lay["btables"] >= 253 and 253 - lay["bbits"] * (lay["btables"] - 1) <= lay["bbits"] - 1
 
 
-def _btab_entries(hc, t, js):
+def _btab_entries(hc, t, js, bits=22):
     import numpy as np
     js = np.asarray(js, np.int32)
     out = np.zeros(32 * len(js), np.int32)
-    assert hc.hc_btab_entries_of(t, js.ctypes.data, len(js), out.ctypes.data) == 0
+    assert hc.hc_btab_entries_of_bits(bits, t, js.ctypes.data, len(js), out.ctypes.data) == 0
     return out.reshape(len(js), 32)
 
 
-def test_btab_entries_are_multiples_of_2_16t_B():
+# the two [S]B table sets (edv_verify_core.h SbShape): large (the default
+# layout above) and compact (16 digits of 16 bits, 64 MiB)
+SB_SHAPES = {22: 12, 16: 16}
+
+
+@pytest.mark.parametrize("bb", sorted(SB_SHAPES))
+def test_btab_entries_are_multiples_of_2_16t_B(bb):
     """Table t of the R side's [S]B: entry j = j x 2^(bbits t) B (affine y+x, y-x,
     2dxy limbs) against the oracle's fixed-base multiplication, for the first,
-    a middle and the last table."""
+    a middle and the last table, in both table sets."""
     import oracle_lib as orc
     hc = hostcheck_lib.load()
-    n = hc.hc_btab_entries()
-    assert n == 2**(hostcheck_lib.layout()["bbits"] - 1) + 1
+    if bb == 22:
+        assert hc.hc_btab_entries() == 2**(hostcheck_lib.layout()["bbits"] - 1) + 1
+    n = 2**(bb - 1) + 1
     d = (-121665 * pow(121666, P - 2, P)) % P
     inv2 = pow(2, P - 2, P)
     r = random.Random(13)
-    nt, bb = hostcheck_lib.layout()["btables"], hostcheck_lib.layout()["bbits"]
+    nt = SB_SHAPES[bb]
+    assert bb * nt >= 253 and 253 - bb * (nt - 1) <= bb - 1
     for t in (0, 1, nt // 2, nt - 1):
         js = [0, 1, 2, 3, 127, 128, 255, 256, 4097, 16384, n - 2, n - 1] + [r.randrange(n) for _ in range(12)]
-        for j, e in zip(js, _btab_entries(hc, t, js)):
+        for j, e in zip(js, _btab_entries(hc, t, js, bb)):
             e = list(e)
             ypx, ymx, xy2d = val(e[0:10]) % P, val(e[10:20]) % P, val(e[20:30]) % P
             y, x = (ypx + ymx) * inv2 % P, (ypx - ymx) * inv2 % P
@@ -298,7 +308,8 @@ def _ed_encode(pt):
     return int.to_bytes(y | ((x & 1) << 255), 32, "little")
 
 
-def test_r_side_point_is_SB_minus_R():
+@pytest.mark.parametrize("bb", sorted(SB_SHAPES))
+def test_r_side_point_is_SB_minus_R(bb):
     """The prep kernel's R side: Q = [S]B - R from the signed radix-2^bbits digits of S,
     against Python affine arithmetic on the oracle's [S]B, for S over the range
     V2 admits (edges and random, below L and below 2^252) and R of every
@@ -308,11 +319,12 @@ def test_r_side_point_is_SB_minus_R():
     hc = hostcheck_lib.load()
     r = random.Random(31)
     out = ctypes.create_string_buffer(32)
-    bb = hostcheck_lib.layout()["bbits"]
+    rside = lambda R, S, o: hc.hc_rside_point_bits(bb, R, S, o)  # noqa: E731
     # digit edges: |d| = 2^(bb-1) (the last entry) with and without carries, all-ones runs
     Ss = [0, 1, 2, 2**bb - 1, 2**bb, 2**(bb - 1), 2**(bb - 1) - 1, 2**(bb - 1) + 1, L - 1, L - 2, 2**252 - 1]
-    Ss += [2**(bb * k) - 1 for k in range(2, 12) if 2**(bb * k) < L] + [2**(bb - 1) * (2**(bb * k) - 1) // (2**bb - 1) % L for k in (3, 11)]
-    Ss += [2**240, 2**252 - 2**240, sum(2**(bb * k + bb - 1) for k in range(11)) % L]
+    nt = SB_SHAPES[bb]
+    Ss += [2**(bb * k) - 1 for k in range(2, nt) if 2**(bb * k) < L] + [2**(bb - 1) * (2**(bb * k) - 1) // (2**bb - 1) % L for k in (3, nt - 1)]
+    Ss += [2**240, 2**252 - 2**240, sum(2**(bb * k + bb - 1) for k in range(nt - 1)) % L]
     Ss += [int("8000" * 16, 16) % L, int("7fff" * 16, 16) % L] + [r.randrange(L) for _ in range(60)]
     pts = []
     for _ in range(8):
@@ -326,11 +338,11 @@ def test_r_side_point_is_SB_minus_R():
         for Rb in pts + ([orc.scalarmult_base(S.to_bytes(32, "little"))] if S else []):  # R = [S]B: Q = identity
             Rp = _ed_decode(Rb)
             want = _ed_encode(_ed_add(sb, ((P - Rp[0]) % P, Rp[1])))
-            assert hc.hc_rside_point(Rb, S.to_bytes(32, "little"), out) == 0, (hex(S), Rb.hex())
+            assert rside(Rb, S.to_bytes(32, "little"), out) == 0, (hex(S), Rb.hex())
             assert out.raw == want, (hex(S), Rb.hex())
     # S with bits above 2^253 (rejected by the hash side): no fault, some point
     for S in (2**256 - 1, 2**255 + 12345, 2**253):
-        assert hc.hc_rside_point(pts[1], S.to_bytes(32, "little"), out) == 0
+        assert rside(pts[1], S.to_bytes(32, "little"), out) == 0
     # rejected R: identity (small order), y >= p (non-canonical), not on the curve
     bad = [_ed_encode((0, 1)), (P + 1).to_bytes(32, "little")]
     y = 2
@@ -338,7 +350,7 @@ def test_r_side_point_is_SB_minus_R():
         y += 1
     bad.append(y.to_bytes(32, "little"))
     for Rb in bad:
-        assert hc.hc_rside_point(Rb, (5).to_bytes(32, "little"), out) == -1, Rb.hex()
+        assert rside(Rb, (5).to_bytes(32, "little"), out) == -1, Rb.hex()
 
 
 N8L = 8 * L

@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU-box session (round 5).  STEP picks the parts (comma list):
+# One GPU-box session (round 6).  STEP picks the parts (comma list):
 #   test    pytest -m gpu + smoke()            (PYTEST_ARGS narrows it)
 #   bench   the default bench.py line           (BENCH_ARGS)
 #   trace   anatomy of synchronous C2 calls (kernel + copy + HIP API traces)
@@ -11,11 +11,11 @@
 #   lds     one --pmc pass of LDS / wait counters over the C2 bench (where the main kernel waits)
 #   extra   $EXTRA (a command line)
 # Every GPU step has its own time limit; the chain stops at the first failure.
-# Outputs land in gpurun_out/r05/<TAG>/.
+# Outputs land in gpurun_out/r06/<TAG>/.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${TAG:-s1}
-O=$R/gpurun_out/r05/$TAG
+O=$R/gpurun_out/r06/$TAG
 mkdir -p $O
 cd $R
 STEP=${STEP:-test,bench}
