@@ -48,9 +48,13 @@ extern "C" {
  * starts as each slice lands), then the main kernel, which writes the
  * verdicts straight into page-locked host memory (no D2H copy).  A larger
  * shard alternates two streams of half-chunk sub-batches, so the copies of
- * one overlap the kernels of the other.  Inputs in pinned memory (e.g. from edv_host_alloc) are copied to the device
- * directly; pageable inputs are first staged through the library's pinned
- * buffers by a parallel memcpy (EDV_COPY_THREADS threads, default 8).
+ * one overlap the kernels of the other.  A shard of at most 8,192 requests
+ * (a Node's prod, one Verifier.verify) takes the latency path instead
+ * (edv_set_latency_path): inputs packed into one pinned block, one DMA, one
+ * kernel launch with four lanes per signature.  Inputs in pinned memory (e.g.
+ * from edv_host_alloc) are copied to the device directly; pageable inputs are
+ * first staged through the library's pinned buffers by a parallel memcpy
+ * (EDV_COPY_THREADS threads, default 8).
  *   sigs     n x 64 bytes (R || S), contiguous
  *   pks      n x 32 bytes (A), contiguous
  *   msgs     concatenated messages; message i = msgs[msg_off[i] .. msg_off[i+1])
@@ -177,6 +181,16 @@ int edv_set_chunk(int device, uint64_t chunk);
  * side runs as soon as it has landed, so only the last slice's remains after
  * the copy.  Tuning knob: verdicts never depend on it. */
 int edv_set_host_slices(int device, int slices);
+
+/* The latency path: every batch of at most max_requests requests (default and
+ * at most 8,192; 0 = never) on `device` -- synchronous, asynchronous and
+ * device-resident calls alike -- runs as ONE kernel launch with four lanes per
+ * signature (edv_quad.hip: each point doubling and addition split over a quad
+ * of lanes, operands exchanged by DPP), one DMA of the packed inputs on the
+ * host paths.  Below one wave per SIMD the batch kernels (one signature per
+ * lane) take a lane's whole serial chain whatever n is; this path divides
+ * that chain instead.  Tuning knob: verdicts never depend on it. */
+int edv_set_latency_path(int device, uint64_t max_requests);
 
 /* SHA-512 length buckets of the device paths (a counting sort of each chunk by
  * block count, so a wave of the prep kernel hashes equally long messages):

@@ -24,6 +24,9 @@ hipError_t launch_comb_kernel(hipStream_t s, int32_t* out);
 hipError_t launch_sign_kernel(unsigned blocks, hipStream_t s, const uint32_t* seeds, const uint8_t* msgs,
                               const uint64_t* off, uint64_t msg_base, uint64_t n, uint32_t* pks, uint32_t* sigs,
                               const int32_t* comb);
+// the latency path (edv_quad.hip): requests base .. base + n - 1 of va in one
+// launch, four lanes per signature; qtab: n x kQSigWords words of scratch
+hipError_t launch_quad_kernel(hipStream_t s, const VerifyArgs& va, int32_t* qtab);
 // accept bytes -> bitmask (ceil(n / 8) bytes)
 hipError_t launch_pack_bits_kernel(hipStream_t s, const uint8_t* acc, uint64_t n, uint8_t* bits);
 hipError_t launch_sha256_kernel(unsigned blocks, hipStream_t s, const uint8_t* msgs, const uint64_t* off,

@@ -21,64 +21,6 @@ namespace {
 // its own latencies), and the two exponentiations no longer sit behind the
 // hash in one lane.
 
-// The R side's view of the [S]B tables: stage() copies the lane's entry
-// straight into the wave's 10 KiB LDS slice (global_load_lds_dwordx4, 64 lanes
-// x 16 B per instruction), so the gather flies during the previous entry's
-// addition without holding registers; fetch() waits and reads it back.  After
-// the last entry the slice holds Q's cached form for the table (put / get).
-constexpr int kBPieces = 8;         // 128-byte entry (30 words used)
-constexpr int kStashPieces = 10;    // cached point, 160 B
-__device__ __forceinline__ void wait_staged() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void wait_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-// BITS: the table set (a compile-time shape: with the shape read at run time
-// the R side's loop kept ~90 more dwords spilled, prep +7 %)
-template <int BITS>
-struct LdsBStage {
-  const int32_t* w;  // the shared tables
-  int32_t* lds;      // the wave's slice: kStashPieces x 64 lanes x 4 words
-  int lane;
-  static constexpr SbShape kShape = BITS == kBBits ? sb_large() : sb_compact();
-  __device__ __forceinline__ SbShape shape() const { return kShape; }
-  __device__ __forceinline__ void stage(int t, int j) {
-    const int32_t* g = w + (size_t(t) * kShape.entries + j) * kBStride;
-#pragma unroll
-    for (int q = 0; q < kBPieces; q++)
-      __builtin_amdgcn_global_load_lds(const_cast<int32_t*>(g + 4 * q), lds + q * 256, 16, 0, 0);
-  }
-  __device__ __forceinline__ ge_precomp fetch() {
-    wait_staged();
-    int32_t v[32];
-#pragma unroll
-    for (int q = 0; q < kBPieces; q++) {
-      const int4 x = reinterpret_cast<const int4*>(lds + q * 256)[lane];
-      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
-    }
-    wait_lds();  // the slice is restaged right after this: the reads must have landed
-    return precomp_from_words(v);
-  }
-  __device__ __forceinline__ void put(const ge_cached& c) {
-    int32_t v[40];
-#pragma unroll
-    for (int l = 0; l < 10; l++) { v[l] = c.YpX.v[l]; v[10 + l] = c.YmX.v[l]; v[20 + l] = c.Z.v[l]; v[30 + l] = c.T2d.v[l]; }
-#pragma unroll
-    for (int q = 0; q < kStashPieces; q++)
-      reinterpret_cast<int4*>(lds + q * 256)[lane] = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-  }
-  __device__ __forceinline__ ge_cached get() const {
-    asm volatile("" ::: "memory");  // read at each use, not once ahead of the loop
-    int32_t v[40];
-#pragma unroll
-    for (int q = 0; q < kStashPieces; q++) {
-      const int4 x = reinterpret_cast<const int4*>(lds + q * 256)[lane];
-      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
-    }
-    ge_cached c;
-#pragma unroll
-    for (int l = 0; l < 10; l++) { c.YpX.v[l] = v[l]; c.YmX.v[l] = v[10 + l]; c.Z.v[l] = v[20 + l]; c.T2d.v[l] = v[30 + l]; }
-    return c;
-  }
-};
-constexpr int kLdsBWaveWords = kStashPieces * 256;
 
 template <int BITS>
 __device__ __forceinline__ void prep_point_side(const VerifyArgs& a, uint64_t j, int side, int32_t* lds) {

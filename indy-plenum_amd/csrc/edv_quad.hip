@@ -1,0 +1,369 @@
+// edv_quad.hip -- the latency path: one kernel launch verifies a small batch
+// (a Node's prod, a single Verifier.verify) with FOUR LANES PER SIGNATURE.
+//
+// The batch path (edv_prep.hip, edv_verify.hip) runs one signature per lane:
+// best for throughput, but a lane's serial chain -- two exponentiations, ~130
+// doublings, ~70 additions, every field product one after the other -- sets
+// the latency of any batch that leaves most of the chip idle (~0.6 ms for
+// n <= 16k: one wave per SIMD at most).  Here a 256-thread workgroup takes 64
+// signatures:
+//
+//   phase 1  wave-specialised (uniform within a wave, so no divergence):
+//              wave 0: V2-V4 byte checks, V6/V7 h = SHA-512(R || A || M) mod L,
+//                      the half-size scalars (a, b) and their digits
+//              wave 1: canonical / small-order checks, decompress -A
+//              wave 2: the same for R
+//              wave 3: [S]B from the shared tables (from identity)
+//            results through LDS, then one barrier;
+//   phase 2  per quad (4 consecutive lanes = one signature): Q = [S]B - R and
+//            the 0..8 x (-A), 0..8 x Q tables, written to global scratch;
+//   phase 3  per quad: the same joint fixed-window walk as the batch path
+//            ([a](-A) + [b](+-Q) == identity), every
+//            point operation split over the quad's lanes.
+//
+// Quad arithmetic.  A point is DISTRIBUTED: lane q of a quad holds coordinate
+// q of (X : Y : Z : T).  The extended-coordinate formulas have four
+// independent field products per stage, so each lane computes one: a doubling
+// is two product latencies (X^2 | Y^2 | 2Z^2 | (X+Y)^2, then X1 T1 | Y1 Z1 |
+// Z1 T1 | X1 Y1) instead of seven, an addition two instead of eight.  The
+// operands a lane needs are gathered from its quad with DPP quad_perm moves
+// (v_mov_b32_dpp / DPP-modified VOP2 adds: the exchange costs a few VOP2 per
+// limb, no LDS); per-lane signs and selects are mask arithmetic (no VCC-mask
+// v_cndmask_b32, ~23 cycles on gfx950).  A table entry is read one coordinate
+// per lane (48-byte slots): the digit's sign picks which slot (YpX <-> YmX)
+// and negates T2d, so no data is selected after the load.
+//
+// Same verdicts as the batch path (same strictness checks, same lattice
+// scalars, same walk), checked against libsodium's golden and corpus verdicts
+// by the GPU tests; the field arithmetic is edv_math.h's.
+#define EDV_NO_SCHED_FENCE 1
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "edv_kernels.h"
+#include "edv_launch.h"
+
+namespace edv {
+namespace {
+
+constexpr int kQSigs = 64;                           // signatures per 256-thread workgroup
+constexpr int kQCoordWords = 12;                     // one coordinate of a table entry, padded to 48 B
+constexpr int kQEntryWords = 4 * kQCoordWords;       // YpX | YmX | T2d | Z
+constexpr int kQTableWords = kAEntries * kQEntryWords;
+static_assert(kQSigWords == 2 * kQTableWords, "edv_kernels.h kQSigWords: tables of -A and Q per signature");
+
+// ------------------------------------------------------------ quad helpers
+constexpr int qp(int a, int b, int c, int d) { return a | (b << 2) | (c << 4) | (d << 6); }
+template <int C>
+__device__ __forceinline__ int32_t dpp(int32_t x) {
+  return __builtin_amdgcn_mov_dpp(x, C, 0xf, 0xf, true);
+}
+template <int C>
+__device__ __forceinline__ fe fdpp(const fe& f) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = dpp<C>(f.v[i]);
+  return r;
+}
+__device__ __forceinline__ fe fand(const fe& f, int32_t m) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = f.v[i] & m;
+  return r;
+}
+// s = 0: f; s = -1: -f
+__device__ __forceinline__ fe fcneg(const fe& f, int32_t s) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = (f.v[i] ^ s) - s;
+  return r;
+}
+// m = -1: a; m = 0: b (v_bfi_b32)
+__device__ __forceinline__ fe fsel(int32_t m, const fe& a, const fe& b) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = (a.v[i] & m) | (b.v[i] & ~m);
+  return r;
+}
+__device__ __forceinline__ fe fshl(const fe& f, int32_t sh) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = f.v[i] << sh;
+  return r;
+}
+
+// Per-lane constants of a quad (opaque, so LLVM keeps them as mask arithmetic)
+struct QLane {
+  int32_t q;           // lane within the quad
+  int32_t m1, m2, m3;  // all ones on lane 1 / 2 / 3
+  int32_t m01;         // all ones on lanes 0 and 1
+  int32_t s1;          // -1 on lane 1
+  int32_t s03, s02;    // -1 on lanes 0, 3 / lanes 0, 2
+  int32_t sh2, sh3;    // 1 on lane 2 / lane 3 (shift amounts)
+  __device__ explicit QLane(int lane) {
+    q = lane & 3;
+    m1 = opaque_i32(-int32_t(q == 1));
+    m2 = opaque_i32(-int32_t(q == 2));
+    m3 = opaque_i32(-int32_t(q == 3));
+    m01 = opaque_i32(-int32_t(q < 2));
+    s1 = m1;
+    s03 = opaque_i32(-int32_t(q == 0 || q == 3));
+    s02 = opaque_i32(-int32_t(q == 0 || q == 2));
+    sh2 = opaque_i32(int32_t(q == 2));
+    sh3 = opaque_i32(int32_t(q == 3));
+  }
+};
+
+// f^2, doubled on lanes where sh = 1 (2 Z^2 for the doubling's lane 2): the
+// unbiased columns are shifted before the rounding bias goes in, so the one
+// biased carry chain reduces either (output bounds of fe_sq)
+__device__ __forceinline__ fe fe_sq_shift(const fe& f, int32_t sh) {
+  int64_t h[10];
+  fe_sq_cols<false, false>(f, h);
+#pragma unroll
+  for (int k = 0; k < 10; k++) h[k] = (h[k] << sh) + bias_reg(k);
+  return fe_carry64_biased(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
+}
+
+// Doubling of a distributed point (dbl-2008-hwcd, a = -1), T ignored on
+// input, all four of X3 Y3 Z3 T3 out.
+__device__ __forceinline__ fe quad_dbl(const fe& p, const QLane& L) {
+  // stage A: X^2 | Y^2 | 2 Z^2 | (X + Y)^2
+  const fe y3 = fand(fdpp<qp(1, 1, 1, 1)>(p), L.m3);   // Y on lane 3
+  const fe u = fe_add(fdpp<qp(0, 1, 2, 0)>(p), y3);     // X | Y | Z | X + Y
+  const fe r = fe_sq_shift(u, L.sh2);
+  // stage B: Y1 = YY + XX, Z1 = YY - XX, X1 = A - Y1, T1 = B - Z1
+  const fe a0 = fdpp<qp(0, 0, 0, 0)>(r), a1 = fdpp<qp(1, 1, 1, 1)>(r);
+  const fe S = fe_add(a1, a0), D = fe_sub(a1, a0);
+  const fe X1 = fe_sub(fdpp<qp(3, 3, 3, 3)>(r), S);
+  const fe T1 = fe_sub(fdpp<qp(2, 2, 2, 2)>(r), D);
+  const fe uu = fsel(L.m1, S, fsel(L.m2, D, X1));  // X1 | Y1 | Z1 | X1
+  const fe vv = fsel(L.m1, D, fsel(L.m3, S, T1));  // T1 | Z1 | T1 | Y1
+  return fe_mul(uu, vv);                           // X3 | Y3 | Z3 | T3
+}
+
+// Addition of a distributed point and one cached-form coordinate per lane
+// (e: YpX | YmX | T2d | Z of the addend, already negated if need be).
+__device__ __forceinline__ fe quad_add(const fe& p, const fe& e, const QLane& L) {
+  // stage A: A = (Y+X) YpX | B = (Y-X) YmX | C = T T2d | ZZ = Z Z'
+  const fe x = fcneg(fand(fdpp<qp(0, 0, 0, 0)>(p), L.m01), L.s1);  // X | -X | 0 | 0
+  const fe u = fe_add(fdpp<qp(1, 1, 3, 2)>(p), x);                   // Y+X | Y-X | T | Z
+  const fe r = fshl(fe_mul(u, e), L.sh3);                            // A | B | C | D = 2 ZZ
+  // stage B: X1 = A - B, Y1 = A + B, Z1 = D + C, T1 = D - C
+  const fe uu = fe_add(fdpp<qp(0, 0, 3, 0)>(r), fcneg(fdpp<qp(1, 1, 2, 1)>(r), L.s03));  // X1 | Y1 | Z1 | X1
+  const fe vv = fe_add(fdpp<qp(3, 3, 3, 0)>(r), fcneg(fdpp<qp(2, 2, 2, 1)>(r), L.s02));  // T1 | Z1 | T1 | Y1
+  return fe_mul(uu, vv);                                                                  // X3 | Y3 | Z3 | T3
+}
+
+// Cached form of a distributed point, one coordinate per lane:
+// YpX | YmX | T2d | Z (the table slot order, quad_add's e)
+__device__ __forceinline__ fe quad_cached(const fe& p, const QLane& L) {
+  const fe x = fcneg(fand(fdpp<qp(0, 0, 0, 0)>(p), L.m01), L.s1);
+  const fe w = fe_add(fdpp<qp(1, 1, 3, 2)>(p), x);  // Y+X | Y-X | T | Z
+  return fe_mul(w, fsel(L.m2, fe_d2(), fe_one()));  // x 1 | x 1 | x 2d | x 1
+}
+
+// the lane's coordinate of a table entry: 10 limbs at a 48-byte slot
+__device__ __forceinline__ void slot_store(int32_t* s, const fe& f) {
+  int4* p = reinterpret_cast<int4*>(s);
+  p[0] = make_int4(f.v[0], f.v[1], f.v[2], f.v[3]);
+  p[1] = make_int4(f.v[4], f.v[5], f.v[6], f.v[7]);
+  p[2] = make_int4(f.v[8], f.v[9], 0, 0);
+}
+__device__ __forceinline__ fe slot_load(const int32_t* s) {
+  const int4* p = reinterpret_cast<const int4*>(s);
+  const int4 a = p[0], b = p[1], c = p[2];
+  return fe{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y}};
+}
+
+// ------------------------------------------------------------ LDS layout
+// per workgroup: phase-1 results for its 64 signatures (structure of arrays:
+// word w of signature j at [w][j]), and wave 3's [S]B staging slice
+constexpr int kQDigWords = 17;  // da[8] | db[8] | nwin | negR << 8
+constexpr int kQPtWords = 40;   // X | Y | Z | T, 10 limbs each
+struct QuadLds {
+  uint32_t dig[kQDigWords][kQSigs];
+  int32_t pt[3][kQPtWords][kQSigs];  // 0: -A, 1: -R, 2: [S]B
+  uint8_t ok[3][kQSigs];              // hash side, A, R
+  int32_t stage[kLdsBWaveWords];      // wave 3: LdsBStage slice
+};
+
+__device__ __forceinline__ void lds_put_point(QuadLds& L, int k, int j, const ge_p3& p) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    L.pt[k][i][j] = p.X.v[i];
+    L.pt[k][10 + i][j] = p.Y.v[i];
+    L.pt[k][20 + i][j] = p.Z.v[i];
+    L.pt[k][30 + i][j] = p.T.v[i];
+  }
+}
+// coordinate q of point k of signature j (the quad's distributed form)
+__device__ __forceinline__ fe lds_coord(const QuadLds& L, int k, int j, int q) {
+  fe f;
+#pragma unroll
+  for (int i = 0; i < 10; i++) f.v[i] = L.pt[k][10 * q + i][j];
+  return f;
+}
+
+// [S]B from identity (wave 3 of phase 1)
+template <int BITS>
+__device__ __forceinline__ ge_p3 sb_point(const uint32_t S[8], const int32_t* btab, int32_t* stage, int lane) {
+  LdsBStage<BITS> bs{btab, stage, lane};
+  ge_p3 q = ge_p3_identity();
+  add_sb(q, S, bs);
+  return q;
+}
+
+// The latency-path kernel: workgroup g verifies requests base + 64 g .. + 63.
+template <int BITS>
+__device__ __forceinline__ void quad_body(const VerifyArgs& a, int32_t* qtab, QuadLds& L) {
+  const int tid = int(threadIdx.x), wave = tid >> 6, lane = tid & 63;
+  const uint64_t g0 = uint64_t(blockIdx.x) * kQSigs;
+  // ---- phase 1: one role per wave, one signature per lane
+  {
+    const uint64_t j = g0 + uint64_t(lane);
+    const bool in = j < a.n;
+    const uint64_t i = a.base + (in ? j : 0);
+    if (wave == 0) {
+      bool ok = false;
+      PrepDigits pd;
+      if (in) {
+        uint32_t R[8], S[8], A[8];
+        load_words(R, a.sigs + 16 * i, 2);
+        load_words(S, a.sigs + 16 * i + 8, 2);
+        load_words(A, a.pks + 8 * i, 2);
+        const uint64_t o0 = a.off[i] - a.msg_base, o1 = a.off[i + 1] - a.msg_base;
+        ok = prep_one(R, S, A, a.msgs + o0, o1 - o0, pd);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        L.dig[k][lane] = ok ? pd.da[k] : 0u;
+        L.dig[8 + k][lane] = ok ? pd.db[k] : 0u;
+      }
+      L.dig[16][lane] = ok ? (uint32_t(pd.nwin) | (pd.negR ? 0x100u : 0u)) : 0u;
+      L.ok[0][lane] = ok ? 1 : 0;
+    } else if (wave == 1 || wave == 2) {
+      uint32_t P[8];
+      bool ok = false;
+      ge_p3 p = ge_p3_identity();
+      if (in) {
+        load_words(P, wave == 1 ? a.pks + 8 * i : a.sigs + 16 * i, 2);
+        ok = ge_is_canonical(P) && !has_small_order(P) && ge_frombytes_negate(p, P);
+        if (!ok) p = ge_p3_identity();
+      }
+      lds_put_point(L, wave - 1, lane, p);
+      L.ok[wave][lane] = ok ? 1 : 0;
+    } else {
+      uint32_t S[8];
+      ge_p3 p = ge_p3_identity();
+      if (in) {
+        load_words(S, a.sigs + 16 * i + 8, 2);
+        p = sb_point<BITS>(S, a.btab, L.stage, lane);
+      }
+      lds_put_point(L, 2, lane, p);
+    }
+  }
+  __syncthreads();
+  // ---- phases 2 and 3: one signature per quad
+  const QLane Q(lane);
+  const int js = tid >> 2;  // signature within the workgroup
+  const uint64_t j = g0 + uint64_t(js);
+  const bool in = j < a.n;
+  const bool alive = in && L.ok[0][js] && L.ok[1][js] && L.ok[2][js];
+  int32_t* tab = qtab + uint64_t(blockIdx.x * kQSigs + js) * kQSigWords;  // tables of -A (0) and Q (1)
+  {
+    // identity entries: YpX = 1, YmX = 1, T2d = 0, Z = 1
+    fe id = fe_zero();
+    id.v[0] = Q.q == 2 ? 0 : 1;
+    slot_store(tab + Q.q * kQCoordWords, id);
+    slot_store(tab + kQTableWords + Q.q * kQCoordWords, id);
+  }
+  // Q = [S]B - R, then 1..8 x Q; 1..8 x (-A)
+#pragma unroll 1
+  for (int t = 1; t >= 0; t--) {
+    fe p;
+    if (t == 1) p = quad_add(lds_coord(L, 2, js, Q.q), quad_cached(lds_coord(L, 1, js, Q.q), Q), Q);
+    else p = lds_coord(L, 0, js, Q.q);
+    int32_t* tt = tab + t * kQTableWords;
+    const fe e1 = quad_cached(p, Q);
+    slot_store(tt + kQEntryWords + Q.q * kQCoordWords, e1);
+    fe cur = quad_dbl(p, Q);
+#pragma unroll 1
+    for (int e = 2; e < kAEntries; e++) {
+      if (e > 2) cur = quad_add(cur, e1, Q);
+      slot_store(tt + e * kQEntryWords + Q.q * kQCoordWords, quad_cached(cur, Q));
+    }
+  }
+  // the tables were written by the quad's lanes: make them visible to their
+  // neighbours (the walk reads the slot its digit's sign selects)
+  __syncthreads();
+  // ---- phase 3: the joint walk, window count = the wave's maximum
+  uint32_t da[8], db[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    da[k] = L.dig[k][js];
+    db[k] = L.dig[8 + k][js];
+  }
+  const uint32_t wf = alive ? L.dig[16][js] : 0u;
+  int nwin = int(wf & 0xff);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nwin = max(nwin, __shfl_xor(nwin, o));
+  nwin = __builtin_amdgcn_readfirstlane(nwin);
+  const bool negR = (wf >> 8) & 1;
+  constexpr int kTop = kAWin * (kAWindows - 1);
+  constexpr int kTopShl = 32 - kAWin - (kTop - 224);
+#pragma unroll 1
+  for (int k = nwin; k < kAWindows; k++) {
+    shl256<kAWin>(da);
+    shl256<kAWin>(db);
+  }
+  // identity, distributed: X = 0 | Y = 1 | Z = 1 | T = 0
+  fe acc = fe_zero();
+  acc.v[0] = (Q.q == 1 || Q.q == 2) ? 1 : 0;
+#pragma unroll 1
+  for (int w = nwin - 1; w >= 0; --w) {
+    const int dA = int32_t(da[7] << kTopShl) >> (32 - kAWin);
+    const int dR = int32_t(db[7] << kTopShl) >> (32 - kAWin);
+    shl256<kAWin>(da);
+    shl256<kAWin>(db);
+    // this lane's slot of each entry: YpX and YmX trade places for a negative
+    // digit, and T2d is negated (below)
+    const bool nA = dA < 0, nR = (dR < 0) != negR;
+    const int cA = Q.q < 2 ? (Q.q ^ int(nA)) : Q.q, cR = Q.q < 2 ? (Q.q ^ int(nR)) : Q.q;
+    fe eA = slot_load(tab + (dA < 0 ? -dA : dA) * kQEntryWords + cA * kQCoordWords);
+    fe eR = slot_load(tab + kQTableWords + (dR < 0 ? -dR : dR) * kQEntryWords + cR * kQCoordWords);
+    if (w != nwin - 1) {
+#pragma unroll 1
+      for (int d = 0; d < kAWin; d++) acc = quad_dbl(acc, Q);
+    }
+    eA = fcneg(eA, opaque_i32(-int32_t(nA && Q.q == 2)));
+    eR = fcneg(eR, opaque_i32(-int32_t(nR && Q.q == 2)));
+    acc = quad_add(acc, eA, Q);
+    acc = quad_add(acc, eR, Q);
+  }
+  // identity: X = 0 (lane 0) and Y - Z = 0 (lane 1)
+  const fe chk = fe_sub(acc, fand(fdpp<qp(0, 2, 2, 2)>(acc), Q.m1));
+  const int32_t z = fe_iszero(chk) ? 1 : 0;
+  const int32_t ok = dpp<qp(0, 0, 0, 0)>(z) & dpp<qp(1, 1, 1, 1)>(z);
+  if (in && Q.q == 0) a.accept[a.base + j] = (alive && ok) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void edv_quad_kernel(VerifyArgs a, int32_t* qtab) {
+  __shared__ QuadLds lds;
+  quad_body<kBBits>(a, qtab, lds);
+}
+__global__ __launch_bounds__(256) void edv_quad_kernel_compact(VerifyArgs a, int32_t* qtab) {
+  __shared__ QuadLds lds;
+  quad_body<kBBitsCompact>(a, qtab, lds);
+}
+
+}  // namespace
+
+hipError_t launch_quad_kernel(hipStream_t s, const VerifyArgs& va, int32_t* qtab) {
+  const unsigned blocks = unsigned((va.n + kQSigs - 1) / kQSigs);
+  if (va.sb.bits == kBBits) edv_quad_kernel<<<dim3(blocks), dim3(256), 0, s>>>(va, qtab);
+  else edv_quad_kernel_compact<<<dim3(blocks), dim3(256), 0, s>>>(va, qtab);
+  return hipGetLastError();
+}
+
+}  // namespace edv

@@ -93,6 +93,13 @@ constexpr int kAsyncSlots = 8;
 // small is one wave per SIMD on a few SIMDs, and its latency (one main-kernel
 // walk, ~0.45 ms) is all it costs.  Larger batches share the chunk scratch.
 constexpr uint64_t kSmallAsync = 8192;
+// The latency path (edv_quad.hip: one launch, four lanes per signature) takes
+// every batch of at most this many requests on the host paths and the
+// device-resident path (edv_set_latency_path changes it per device; 0 = off).
+// Below one wave per SIMD the batch kernels' time is one lane's serial chain
+// whatever n is; the quad kernel splits each point operation over four lanes.
+constexpr uint64_t kQuadMaxDefault = 8192;  // profiles/r06/latency_paths_s3.jsonl: faster than the batch kernels at every n up to 8,192
+constexpr uint64_t kQuadMaxLimit = kSmallAsync;  // the async slots' scratch is sized for it
 
 // One set of per-chunk state buffers (ChunkState storage + bucket permutation)
 // for `cap` signatures (~5.5 kB each: ~1.4 GB for a whole 2^18 chunk).  Sized
@@ -134,6 +141,7 @@ struct DevCtx {
   int32_t* comb = nullptr;         // signer comb table, built on first edv_sign_* call
   uint64_t chunk = kChunkDefault;  // EDV_CHUNK overrides (tests exercise chunk seams)
   int length_buckets = 2;          // 0 never, 1 always, 2 auto (edv_set_length_buckets)
+  uint64_t quad_max = kQuadMaxDefault;  // latency path up to this batch size (edv_set_latency_path)
   ChunkBufs st;                    // scratch of the ordinary paths
   // st_done: recorded after the last kernel that used `st`, on whatever stream
   // that was; every later user waits for it first, so launches on different
@@ -163,6 +171,7 @@ struct DevCtx {
     bool dig_pinned = false;     // digests DMA'd straight into `digests`
     hipStream_t st = nullptr;    // small batches: copies, kernels and D2H all on this stream
     ChunkBufs cb;                // small batches: the slot's own chunk scratch (grown to the batch)
+    DevBuf qtab;                 // latency-path batches: the quad kernel's table scratch
 #ifdef EDV_MEASUREMENT_API
     bool injected = false;       // edv_test_fail_async: this batch launched nothing and fails
 #endif
@@ -174,6 +183,11 @@ struct DevCtx {
   AsyncLedger ledger;
   DevBuf sigs, pks, msgs, off, acc;
   DevBuf fblob;  // the field path's signatures | keys | offsets block when they arrive in one copy
+  // latency path of the synchronous and device-resident calls: packed inputs
+  // (one DMA) and the quad kernel's table scratch (ordered by st_done, like
+  // the chunk scratch)
+  DevBuf qblob, qtab;
+  PinnedBuf qstage;
   PinnedBuf stage[kQ], acc_host;
   // Pipelined submission (edv_verify_batch_dev_pipelined): two state sets, a
   // prep stream and a main stream, so the prep kernel of batch k+1 runs on the
@@ -455,6 +469,40 @@ bool bucketing_enabled(const DevCtx& c, uint32_t flags) {
   return c.length_buckets != 0;
 }
 
+// ---- the latency path (edv_quad.hip)
+// The quad kernel over n requests whose inputs are device pointers (offsets
+// absolute, minus msg_base), verdicts to d_acc[0, n); qtab is this launch's
+// scratch (the caller orders it against its previous user).
+int launch_quad(DevCtx& c, DevBuf& qtab, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
+                const uint64_t* d_off, uint64_t msg_base, uint64_t n, uint8_t* d_acc, hipStream_t s) {
+  if (n == 0) return 0;
+  // the last workgroup's 64 quads all write their tables, in range or not
+  if (qtab.ensure((n + 63) / 64 * 64 * kQSigWords * 4)) return EDV_E_OOM;
+  VerifyArgs va;
+  memset(&va, 0, sizeof va);
+  va.sigs = reinterpret_cast<const uint32_t*>(d_sigs);
+  va.pks = reinterpret_cast<const uint32_t*>(d_pks);
+  va.msgs = d_msgs;
+  va.off = d_off;
+  va.msg_base = msg_base;
+  va.base = 0;
+  va.n = n;
+  va.accept = d_acc;
+  pick_tables(c, n, &va.btab, &va.sb);
+#ifdef EDV_MEASURE_NO_VERIFY
+  HIPOK(hipMemsetAsync(d_acc, 1, n, s), "memset accept");  // measurement build: see launch_main
+  return 0;
+#endif
+  HIPOK(launch_quad_kernel(s, va, static_cast<int32_t*>(qtab.p)), "quad launch");
+  return 0;
+}
+// A packed block (quad_pack) on the device at d_blob
+int launch_quad_packed(DevCtx& c, DevBuf& qtab, const uint8_t* d_blob, uint64_t n, uint64_t msg_base, uint8_t* d_acc,
+                       hipStream_t s) {
+  return launch_quad(c, qtab, d_blob, d_blob + 64 * n, d_blob + 96 * n + 8 * (n + 1),
+                     reinterpret_cast<const uint64_t*>(d_blob + 96 * n), msg_base, n, d_acc, s);
+}
+
 // Ordinary device path: launch on stream s; caller holds c.mu.  The batch is
 // walked in chunks of c.chunk signatures: [length buckets,] prep kernel, main
 // kernel, all in stream order, after every earlier user of the scratch.
@@ -463,6 +511,12 @@ int launch(DevCtx& c, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t
   if (n == 0) return 0;
   const bool bucket = bucketing_enabled(c, flags);
   int err;
+  if (n <= c.quad_max) {  // the latency path, its scratch ordered like the chunk scratch
+    HIPOK(hipStreamWaitEvent(s, c.st_done, 0), "wait scratch");
+    if ((err = launch_quad(c, c.qtab, d_sigs, d_pks, d_msgs, d_off, msg_base, n, d_accept, s))) return err;
+    HIPOK(hipEventRecord(c.st_done, s), "record scratch");
+    return 0;
+  }
   if ((err = grow_state(c, n))) return err;
   HIPOK(hipStreamWaitEvent(s, c.st_done, 0), "wait scratch");
   VerifyArgs va = make_args(c, c.st, d_sigs, d_pks, d_msgs, d_off, msg_base, d_accept, bucket, 0, n);
@@ -650,6 +704,20 @@ void par_copy(const std::vector<Seg>& segs) {
   for (auto& x : th) x.join();
 }
 
+// One pinned block per batch: signatures | keys | offsets | messages (+ 64
+// bytes of read slack), copied to the device in ONE DMA (each separate copy
+// costs the DMA engine a gap, trace_sync); signatures and keys stay 16-byte
+// aligned, offsets 8-byte aligned.
+uint64_t quad_pack_bytes(uint64_t n, uint64_t mbytes) { return 96 * n + 8 * (n + 1) + mbytes + 64; }
+void quad_pack(uint8_t* dst, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
+               uint64_t lo, uint64_t hi) {
+  const uint64_t n = hi - lo, mbase = off[lo], mbytes = off[hi] - mbase;
+  par_copy({{dst, sigs + 64 * lo, 64 * n},
+            {dst + 64 * n, pks + 32 * lo, 32 * n},
+            {dst + 96 * n, reinterpret_cast<const uint8_t*>(off + lo), 8 * (n + 1)},
+            {dst + 96 * n + 8 * (n + 1), mbytes ? msgs + mbase : nullptr, mbytes}});
+  memset(dst + 96 * n + 8 * (n + 1) + mbytes, 0, 64);
+}
 // memcpy of src[0, bounds[K]) into pinned staging over copy_threads() threads,
 // part by part (part k = [bounds[k], bounds[k+1])), with part k's DMA to the
 // device queued on stream s -- and ev[k], if given, recorded after it -- as
@@ -872,6 +940,41 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
   return 0;
 }
 
+// The latency path of a synchronous call (a shard of at most c.quad_max
+// requests): pack the inputs into the pinned block (a memcpy of a few hundred
+// kB for a Node's prod), one DMA, the quad kernel, verdicts written straight
+// into page-locked host memory.  Caller holds c.mu.
+int run_shard_quad(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
+                   uint64_t lo, uint64_t hi, uint8_t* accept) {
+  const uint64_t n = hi - lo, mbase = off[lo], bytes = quad_pack_bytes(n, off[hi] - mbase);
+  const hipStream_t s = c.hs[0];
+  if (hipEventQuery(c.st_done) != hipSuccess) {  // the scratch's previous user (any stream)
+    (void)hipGetLastError();
+    HIPOK(hipStreamWaitEvent(s, c.st_done, 0), "wait scratch");
+  }
+  if (c.qstage.ensure(bytes) || c.qblob.ensure(bytes)) return EDV_E_OOM;
+  uint8_t* blob = static_cast<uint8_t*>(c.qstage.p);
+  quad_pack(blob, sigs, pks, msgs, off, lo, hi);
+  HIPOK(hipMemcpyAsync(c.qblob.p, blob, bytes, hipMemcpyHostToDevice, s), "h2d packed");
+  const bool acc_pinned = is_pinned(accept + lo);
+  if (!acc_pinned && c.acc_host.ensure(n)) return EDV_E_OOM;
+  uint8_t* h_acc = acc_pinned ? accept + lo : static_cast<uint8_t*>(c.acc_host.p);
+  void* zc = nullptr;
+  if (hipHostGetDevicePointer(&zc, h_acc, 0) != hipSuccess || !zc) {
+    (void)hipGetLastError();
+    zc = nullptr;
+    if (c.acc.ensure(n)) return EDV_E_OOM;
+  }
+  uint8_t* d_acc = zc ? static_cast<uint8_t*>(zc) : static_cast<uint8_t*>(c.acc.p);
+  int err;
+  if ((err = launch_quad_packed(c, c.qtab, static_cast<uint8_t*>(c.qblob.p), n, mbase, d_acc, s))) return err;
+  if (!zc) HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, s), "d2h accept");
+  HIPOK(hipEventRecord(c.st_done, s), "record scratch");
+  HIPOK(hipStreamSynchronize(s), "stream sync");
+  if (!acc_pinned) memcpy(accept + lo, h_acc, n);
+  return 0;
+}
+
 // One shard on one device, host buffers: sub-batches of P requests go round
 // robin over the kQ host-path streams; per sub-batch: H2D copies (straight
 // from the caller's memory when it is pinned, else through this stream's
@@ -885,6 +988,7 @@ int run_shard(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t*
               uint64_t hi, uint8_t* accept, int uniform) {
   const uint64_t n = hi - lo;
   if (n == 0) return 0;
+  if (n <= c.quad_max) return run_shard_quad(c, sigs, pks, msgs, off, lo, hi, accept);
   // A shard that fits one chunk is one sub-batch (the field path): split 2 or
   // 4 ways at 64k it measured 1.6x / 1.9x slower (profiles/r02/e2e_probe_s4.json),
   // as a 16k sub-batch still takes a whole batch's latency at one wave per
@@ -1033,6 +1137,57 @@ int async_complete(DevCtx& c, DevCtx::AsyncSlot& s) {
   return 0;
 }
 
+// An asynchronous latency-path batch on slot s (ticket t, the slot's previous
+// batch complete): packed into the slot's pinned staging, one DMA and the quad
+// kernel on the slot's own stream, verdicts (and digests) as submit_async's.
+int submit_async_quad(DevCtx& c, DevCtx::AsyncSlot& s, int64_t t, const uint8_t* sigs, const uint8_t* pks,
+                      const uint8_t* msgs, const uint64_t* off, uint64_t n, uint8_t* accept, uint8_t* digests,
+                      int64_t* ticket) {
+  const uint64_t mbase = off[0], bytes = quad_pack_bytes(n, off[n] - mbase);
+  if (!s.st) HIPOK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking), "hipStreamCreate");
+  if (s.stage.ensure(bytes) || s.msgs.ensure(bytes) || s.acc.ensure(n) || (digests && s.dig.ensure(32 * n)))
+    return EDV_E_OOM;
+  s.dig_pinned = digests && is_pinned(digests);
+  if (digests && !s.dig_pinned && s.dig_host.ensure(32 * n)) return EDV_E_OOM;
+  s.acc_pinned = is_pinned(accept);
+  if (!s.acc_pinned && s.acc_host.ensure(n)) return EDV_E_OOM;
+  uint8_t* blob = static_cast<uint8_t*>(s.stage.p);
+  quad_pack(blob, sigs, pks, msgs, off, 0, n);
+  uint8_t* d_blob = static_cast<uint8_t*>(s.msgs.p);
+  HIPOK(hipMemcpyAsync(d_blob, blob, bytes, hipMemcpyHostToDevice, s.st), "h2d packed");
+  uint8_t* h_acc = s.acc_pinned ? accept : static_cast<uint8_t*>(s.acc_host.p);
+  void* zc = nullptr;
+  if (hipHostGetDevicePointer(&zc, h_acc, 0) != hipSuccess || !zc) {
+    (void)hipGetLastError();
+    zc = nullptr;
+  }
+  uint8_t* d_acc = zc ? static_cast<uint8_t*>(zc) : static_cast<uint8_t*>(s.acc.p);
+  bool skip = false;  // edv_test_fail_async (measurement build): no kernels, and the wait fails
+#ifdef EDV_MEASUREMENT_API
+  skip = s.injected = (t == c.inject_fail);
+#endif
+  int err;
+  if (!skip && (err = launch_quad_packed(c, s.qtab, d_blob, n, mbase, d_acc, s.st))) return err;
+  if (!zc) HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, s.st), "d2h accept");
+  if (digests && !skip) {
+    // Request.getDigest of requests whose signing bytes ARE the message (the
+    // caller decides which): SHA-256 of the message bytes already on the device
+    uint8_t* d_dig = static_cast<uint8_t*>(s.dig.p);
+    if ((err = launch_sha256(d_blob + 96 * n + 8 * (n + 1), reinterpret_cast<const uint64_t*>(d_blob + 96 * n), mbase,
+                             n, d_dig, s.st)))
+      return err;
+    uint8_t* h_dig = s.dig_pinned ? digests : static_cast<uint8_t*>(s.dig_host.p);
+    HIPOK(hipMemcpyAsync(h_dig, d_dig, 32 * n, hipMemcpyDeviceToHost, s.st), "d2h digests");
+  }
+  HIPOK(hipEventRecord(s.done, s.st), "record");
+  s.ticket = t;
+  s.accept = accept;
+  s.digests = digests;
+  s.n = n;
+  *ticket = c.ledger.issue();
+  return 0;
+}
+
 // Queue one host batch: H2D copies on hcp (from the caller's memory when it is
 // pinned, else through the slot's pinned staging, filled here while the
 // previous batch computes), then on hac the kernels and the D2H of the
@@ -1052,6 +1207,8 @@ int submit_async(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8
   if (s.sigs.ensure(n * 64) || s.pks.ensure(n * 32) || s.msgs.ensure(mbytes + 64) || s.off.ensure((n + 1) * 8) ||
       s.acc.ensure(n) || (digests && s.dig.ensure(32 * n)))
     return EDV_E_OOM;
+  // the latency path: the slot's pinned staging packed, one DMA, the quad kernel
+  if (n <= c.quad_max) return submit_async_quad(c, s, t, sigs, pks, msgs, off, n, accept, digests, ticket);
   // small batch: everything on the slot's stream and scratch (see kSmallAsync)
   const bool own = n <= kSmallAsync;
   if (own) {
@@ -1355,9 +1512,10 @@ int edv_context_memory(int device, uint64_t out[7]) {
   out[1] = shared_tables_bytes(c->phys);
   out[2] = c->st.bytes();
   for (const auto& a : c->as)
-    out[3] += a.sigs.cap + a.pks.cap + a.msgs.cap + a.off.cap + a.acc.cap + a.dig.cap + a.cb.bytes();
+    out[3] += a.sigs.cap + a.pks.cap + a.msgs.cap + a.off.cap + a.acc.cap + a.dig.cap + a.cb.bytes() + a.qtab.cap;
   out[4] = c->pst[0].bytes() + c->pst[1].bytes();
-  out[5] = c->sigs.cap + c->pks.cap + c->msgs.cap + c->off.cap + c->acc.cap + c->fblob.cap;
+  out[5] = c->sigs.cap + c->pks.cap + c->msgs.cap + c->off.cap + c->acc.cap + c->fblob.cap + c->qblob.cap +
+           c->qtab.cap;
   out[6] = c->comb ? uint64_t(kCombRows) * kCombEntries * kBStride * 4 : 0;
   for (int k = 1; k < 7; k++) out[0] += out[k];
   return 0;
@@ -1626,6 +1784,17 @@ int edv_set_host_slices(int device, int slices) {
   if (slices < 0 || slices > kSlices) return set_err(EDV_E_ARG, "slices must be 0..8");
   std::lock_guard<std::mutex> lk(c->mu);
   c->host_slices = slices;
+  return 0;
+}
+
+int edv_set_latency_path(int device, uint64_t max_requests) {
+  g_err.clear();
+  int err = 0;
+  DevCtx* c = get_ctx(device, &err);
+  if (!c) return err;
+  if (max_requests > kQuadMaxLimit) return set_err(EDV_E_ARG, "latency path is for batches of at most 8,192");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->quad_max = max_requests;
   return 0;
 }
 

@@ -695,11 +695,10 @@ EDV_HD void shr256_var(uint32_t v[8], int n) {  // 0 < n < 32
   for (int i = 0; i < 7; i++) v[i] = (v[i] >> n) | (v[i + 1] << (32 - n));
   v[7] >>= n;
 }
-// Q = [S]B - R (projective) for a decodable R; false if R is rejected
+// q += [S]B: the sh.tables mixed additions of the signed radix-2^sh.bits
+// digits of S (cut to 253 bits) against BTab's tables
 template <class BTab>
-EDV_HD bool rpoint_q(const uint32_t R[8], const uint32_t S[8], BTab& bt, ge_p3& q) {
-  if (!ge_is_canonical(R) || has_small_order(R)) return false;
-  if (!ge_frombytes_negate(q, R)) return false;
+EDV_HD void add_sb(ge_p3& q, const uint32_t S[8], BTab& bt) {
   const SbShape sh = bt.shape();
   uint32_t s[8];
 #pragma unroll
@@ -728,6 +727,13 @@ EDV_HD bool rpoint_q(const uint32_t R[8], const uint32_t S[8], BTab& bt, ge_p3& 
     }
     q = ge_p1p1_to_p3(ge_madd(q, e));
   }
+}
+// Q = [S]B - R (projective) for a decodable R; false if R is rejected
+template <class BTab>
+EDV_HD bool rpoint_q(const uint32_t R[8], const uint32_t S[8], BTab& bt, ge_p3& q) {
+  if (!ge_is_canonical(R) || has_small_order(R)) return false;
+  if (!ge_frombytes_negate(q, R)) return false;
+  add_sb(q, S, bt);
   return true;
 }
 template <class ATab, class BTab>

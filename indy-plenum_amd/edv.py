@@ -102,6 +102,8 @@ def lib():
         h.edv_stream.restype = ctypes.c_int
         h.edv_sync.argtypes = [ctypes.c_int]
         h.edv_sync.restype = ctypes.c_int
+        h.edv_set_latency_path.argtypes = [ctypes.c_int, u64]
+        h.edv_set_latency_path.restype = ctypes.c_int
         h.edv_set_length_buckets.argtypes = [ctypes.c_int, ctypes.c_int]
         h.edv_set_length_buckets.restype = ctypes.c_int
         h.edv_set_chunk.argtypes = [ctypes.c_int, u64]
@@ -231,6 +233,15 @@ def sync(device: int = 0):
 def set_length_buckets(device: int, mode: int):
     """SHA-512 length buckets on the device paths: 0 never, 1 always, 2 auto (default)."""
     _check(lib().edv_set_length_buckets(device, mode))
+
+
+LATENCY_PATH_DEFAULT = 8192
+
+
+def set_latency_path(device: int, max_requests: int):
+    """Batches of at most max_requests (0 = never) run on the four-lanes-per-
+    signature latency kernel (edv_set_latency_path).  Never changes verdicts."""
+    _check(lib().edv_set_latency_path(device, max_requests))
 
 
 def set_chunk(device: int, chunk: int):

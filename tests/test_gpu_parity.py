@@ -127,13 +127,15 @@ def test_long_and_skewed_message_lengths():
     sigs, pks, msgs, off = _signed_lengths(lens, 0x5A)
     want = checker(sigs, pks, msgs, off)
     assert 0.65 < want.mean() < 0.95
-    assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off), want)
+    assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off), want)   # the latency path (n <= 8,192)
     try:
-        for chunk in (256, 1024):
+        edv.set_latency_path(0, 0)   # the batch kernels, across chunk seams
+        for chunk in (256, 1024, 0):
             edv.set_chunk(0, chunk)
             assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off), want), chunk
     finally:
         edv.set_chunk(0, 0)
+        edv.set_latency_path(0, edv.LATENCY_PATH_DEFAULT)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
@@ -142,12 +144,14 @@ def test_chunk_seams(mode):
     (200..4096 B) also exercises the per-chunk SHA length buckets."""
     sigs, pks, msgs, off = orc.corpus(0x5EA + mode, 0, 5000, mode=mode, invalid_permille=200)
     want = checker(sigs, pks, msgs, off)
+    edv.set_latency_path(0, 0)   # the batch kernels (5,000 requests would take the latency path)
     try:
         for chunk in (256, 768, 4096):
             edv.set_chunk(0, chunk)
             assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off), want), chunk
     finally:
         edv.set_chunk(0, 0)  # back to the default
+        edv.set_latency_path(0, edv.LATENCY_PATH_DEFAULT)
 
 
 def test_fuzzed_damage_vs_libsodium():
@@ -393,8 +397,90 @@ def test_length_bucket_modes_same_verdicts(mode):
         b.upload(a)
     acc = edv.DeviceBuffer(3000)
     try:
+        edv.set_latency_path(0, 0)   # the batch kernels, where the buckets apply
         edv.set_length_buckets(0, mode)
         edv.verify_device(bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, 3000, acc.ptr)
         assert np.array_equal(acc.download(3000), want)
     finally:
         edv.set_length_buckets(0, 2)
+        edv.set_latency_path(0, edv.LATENCY_PATH_DEFAULT)
+
+
+# ---- the latency path (edv_quad.hip): four lanes per signature, one launch
+@pytest.fixture
+def latency_limit():
+    """Set the latency path's batch limit of device 0 for one test, restored after."""
+    def setter(limit):
+        edv.set_latency_path(0, limit)
+    yield setter
+    edv.set_latency_path(0, edv.LATENCY_PATH_DEFAULT)
+
+
+@pytest.mark.parametrize("limit", [0, 8192])
+def test_golden_on_both_paths(golden, golden_meta, latency_limit, limit):
+    """The 3,284 libsodium golden cases (every strictness category: S + kL,
+    torsion and mixed-order A accepted iff 8 | h, small-order and non-canonical
+    R / A, off-curve points, ...) on the batch kernels (limit 0) and on the
+    latency kernel (limit 8,192: the whole set in one launch), and the
+    positional-split cases through open_batch."""
+    latency_limit(limit)
+    sigs, pks, msgs, off = golden_io.pack_batch(golden)
+    got = edv.verify_arrays(sigs, pks, msgs + b"\0" * 16, off)
+    want = np.array([g[0] for g in golden], dtype=np.uint8)
+    cats = golden_meta["categories"]
+    assert [(int(i), cats[golden[i][1]]) for i in np.nonzero(got != want)[0]] == []
+    rows = golden_io.load_open_golden()
+    assert edv.open_batch([(s, m, p) for s, m, p, _a in rows]) == [bool(a) for *_x, a in rows]
+
+
+def test_latency_path_batch_sizes_and_entry_points(latency_limit):
+    """Batch sizes around the quad kernel's 64-signature workgroups and its
+    limit, variable message lengths (200..4,096 B) and 20 % damage, through the
+    synchronous call, the asynchronous one (pageable and page-locked verdicts)
+    and the device-resident one with a non-zero msg_base; verdicts equal
+    libsodium's (the oracle where it is absent)."""
+    latency_limit(8192)
+    sigs, pks, msgs, off = orc.corpus(0x1A7, 0, 8192, mode=1, invalid_permille=200)
+    want = checker(sigs, pks, msgs, off)
+    for n in (1, 2, 3, 4, 5, 63, 64, 65, 127, 128, 129, 400, 1000, 4095, 4096, 4097, 8192):
+        o = off[:n + 1]
+        got = edv.verify_arrays(sigs[:64 * n], pks[:32 * n], msgs, o)
+        assert np.array_equal(got, want[:n]), n
+    pin = edv.PinnedBuffer(8192)
+    for n, acc in ((400, np.zeros(400, np.uint8)), (8192, pin.array[:8192])):
+        ts = [edv.verify_async(sigs[:64 * n], pks[:32 * n], msgs, off[:n + 1], acc) for _ in range(1)]
+        for t in ts:
+            edv.wait_async(t)
+        assert np.array_equal(acc, want[:n]), n
+    pin.free()
+    # device resident: requests [1000, 3000) with the global offsets and msg_base
+    o = off[1000:3001].copy()
+    bufs = [edv.DeviceBuffer(x.nbytes + 64) for x in (sigs[64000:192000], pks[32000:96000],
+                                                      msgs[int(o[0]):int(o[-1])], o)]
+    for b, x in zip(bufs, (sigs[64000:192000], pks[32000:96000], msgs[int(o[0]):int(o[-1])], o)):
+        b.upload(x)
+    acc = edv.DeviceBuffer(2000)
+    acc.upload(np.full(2000, 7, np.uint8))
+    edv.verify_device(bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, 2000, acc.ptr, msg_base=int(o[0]))
+    assert np.array_equal(acc.download(2000), want[1000:3000])
+
+
+def test_latency_path_on_corpus_bitmask_slices(latency_limit):
+    """The latency kernel against libsodium's committed corpus bitmasks: the
+    first 2^18 requests of the C2 corpus (256 B) and of the C4 corpus
+    (200..4,096 B, 5 % invalid over every damage kind), in 4,096-request calls
+    (the default limit), slice hashes checked first."""
+    latency_limit(4096)
+    meta = _bitmask_meta()
+    for name in ("c2_256B", "c4_var"):
+        cfg = meta["corpora"][name]
+        n = 262144
+        sigs, pks, msgs, off = orc.corpus(cfg["seed"], 0, n, cfg["mode"], cfg["invalid_permille"])
+        bits = np.fromfile(os.path.join(GOLDEN, "corpus_%s.bits" % name), dtype=np.uint8)
+        want = np.unpackbits(bits[:n // 8], bitorder="little")
+        got = np.zeros(n, np.uint8)
+        for lo in range(0, n, 4096):
+            got[lo:lo + 4096] = edv.verify_arrays(sigs[64 * lo:64 * (lo + 4096)], pks[32 * lo:32 * (lo + 4096)],
+                                                  msgs, off[lo:lo + 4097])
+        mism = np.nonzero(got != want)[0]
+        assert mism.size == 0, (name, mism[:10].tolist())

@@ -32,6 +32,18 @@ def gpu_present():
     assert edv.device_count() >= 1, "no gfx950 device visible: the GPU suite must run on the MI355X box"
 
 
+@pytest.fixture(autouse=True)
+def batch_kernels_for_small_batches():
+    """This module tests the batch kernels' host-path mechanics (field slices,
+    sub-batches, chunk seams, slot streams) on batches that the latency path
+    (edv_set_latency_path, default: up to 8,192 requests) would otherwise take:
+    here it is off on device 0; test_gpu_parity.py and the fault-hook test
+    below cover the latency path."""
+    edv.set_latency_path(0, 0)
+    yield
+    edv.set_latency_path(0, edv.LATENCY_PATH_DEFAULT)
+
+
 def checker(sigs, pks, msgs, off):
     if orc.sodium_batch() is not None:
         return orc.sodium_verify_batch(sigs, pks, msgs, off, 16)
