@@ -726,20 +726,60 @@ def node_path_leg(n=65536, reps=3):
                                      "one GPU SHA-256 batch"}}
 
 
-def timed_steps(step, drain, steps, reps, rdv, only_rank=None, own=None):
+class StreamEvents:
+    """HIP events on a HIP stream, through the runtime libedv.so itself links
+    (libamdhip64.so.7: one runtime in the process): bracket the timed steps on
+    the stream the kernels are launched on, so the kernels' own GPU time of the
+    timed region is measured live, not re-measured in a separate profile."""
+
+    def __init__(self):
+        import ctypes
+        self.ct = ctypes
+        self.hip = ctypes.CDLL("libamdhip64.so.7")
+        self.hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self.hip.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+        self.hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+        self.hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        self.ev = []
+        for _ in range(2):
+            e = ctypes.c_void_p()
+            assert self.hip.hipEventCreate(ctypes.byref(e)) == 0
+            self.ev.append(e)
+
+    def start(self, stream):
+        assert self.hip.hipEventRecord(self.ev[0], self.ct.c_void_p(stream)) == 0
+
+    def stop(self, stream):
+        assert self.hip.hipEventRecord(self.ev[1], self.ct.c_void_p(stream)) == 0
+
+    def elapsed_ms(self):
+        assert self.hip.hipEventSynchronize(self.ev[1]) == 0
+        ms = self.ct.c_float(0)
+        assert self.hip.hipEventElapsedTime(self.ct.byref(ms), self.ev[0], self.ev[1]) == 0
+        return float(ms.value)
+
+
+def timed_steps(step, drain, steps, reps, rdv, only_rank=None, own=None, events=None):
     """R repetitions of `steps` steps, each between barrier + sync; max over
     ranks per repetition -> list of seconds.  only_rank: that rank alone runs
     the steps (the others wait at the barriers).  own: gets this rank's time of
-    each repetition."""
+    each repetition.  events: (StreamEvents, stream, list) -- the GPU time of
+    each repetition's steps on that stream is appended to the list (ms)."""
     out = []
     for _ in range(max(1, reps)):
         drain()
         rdv.barrier()
         t0 = time.perf_counter()
         if only_rank is None or rdv.rank == only_rank:
+            if events:
+                events[0].start(events[1])
             for _ in range(steps):
                 step()
+            if events:
+                events[0].stop(events[1])
             drain()
+            if events:
+                events[2].append(events[0].elapsed_ms())
         t1 = time.perf_counter()
         rdv.barrier()
         if own is not None:
@@ -934,15 +974,19 @@ def main():
         # the same workload on one GPU: rank 0 times its own shard while the other
         # ranks wait at the barrier (one repetition of K steps), before the joint reps
         alone = timed_steps(step, drain, args.steps, 1, rdv, only_rank=0)[0]
-    mine_s = []
-    reps = timed_steps(step, drain, args.steps, args.reps, rdv, own=mine_s)
+    mine_s, gpu_ms = [], []
+    # the kernels' GPU time inside the timed region: HIP events on the library
+    # stream bracketing each repetition's steps (sequential mode: every kernel
+    # of a step is on that stream)
+    evs = None if args.pipeline else (StreamEvents(), s, gpu_ms)
+    reps = timed_steps(step, drain, args.steps, args.reps, rdv, own=mine_s, events=evs)
     elapsed = statistics.median(reps)
     ms_step = 1e3 * elapsed / args.steps
     value = total * args.steps / elapsed
     per_rank_s = [struct.unpack("<d", g)[0] for g in rdv.gather(struct.pack("<d", statistics.median(mine_s)))]
 
-    # per-kernel durations (HIP events on the kernels' own stream) on the first
-    # chunk-sized slice of this rank's batch
+    # the prep / main split of a launch pair (libedv_measure.so: each kernel
+    # between HIP events, on the first chunk-sized slice of this rank's batch)
     pn = min(n, 1 << 18)
     iters = max(3, min(args.steps, 10))
     prep_ms, main_ms = edv.profile_device(batch.d_sigs.ptr, batch.d_pks.ptr, batch.d_msgs.ptr, batch.d_off.ptr, pn,
@@ -970,7 +1014,11 @@ def main():
         rdv.close()
         return
 
-    path_ms = prep_ms + main_ms
+    # per launch pair (pn requests): the timed region's own GPU time when the
+    # events bracketed it, else the profile's sum
+    pairs_per_step = n / pn
+    pair_ms_timed = statistics.median(gpu_ms) / (args.steps * pairs_per_step) if gpu_ms else None
+    path_ms = pair_ms_timed if pair_ms_timed is not None else prep_ms + main_ms
     ops = w_total(args.msg_len) * pn
     achieved = ops / (path_ms * 1e-3)
     # SURVEY 8d's whole-job fraction: the job's verifies/s x W(m) over N GPUs' peak
@@ -986,9 +1034,15 @@ def main():
                 "traffic": None, "traffic_unit": "bytes/launch pair",
                 "traffic_source": why, "algorithmic_bytes": (64 + 32 + args.msg_len + 8 + 1) * pn,
                 "ops_per_launch": ops, "kernel_ms": path_ms, "prep_kernel_ms": prep_ms, "main_kernel_ms": main_ms,
+                "kernel_ms_source": ("HIP events on the library stream around each timed repetition's %d steps "
+                                     "(median repetition), per prep + main launch pair" % args.steps
+                                     if pair_ms_timed is not None else "prep + main profile (libedv_measure.so)"),
+                "profile_pair_ms": prep_ms + main_ms,
+                "profile_what": "prep_kernel_ms / main_kernel_ms: each kernel alone between HIP events "
+                                "(libedv_measure.so, %d launch pairs, a sync after each)" % iters,
                 "vop2_issue_peak": PEAK_VOP2 / 1e12,
-                "convention": "achieved = SURVEY 8d W(m) INT32 ops per verify x verifies / (prep + main HIP-event "
-                              "kernel time); peak = 256 CU x 64 lanes x 2.4 GHz (4-cycle VOP3 issue)"}
+                "convention": "achieved = SURVEY 8d W(m) INT32 ops per verify x verifies per launch pair / the pair's "
+                              "GPU time; peak = 256 CU x 64 lanes x 2.4 GHz (4-cycle VOP3 issue)"}
     if pmc:
         roofline.update(pmc)
         if "dram_bytes_per_verify_upper_bound" in pmc:

@@ -78,11 +78,17 @@ __device__ __forceinline__ fe fcneg(const fe& f, int32_t s) {
   for (int i = 0; i < 10; i++) r.v[i] = (f.v[i] ^ s) - s;
   return r;
 }
-// m = -1: a; m = 0: b (v_bfi_b32)
+// m = -1: a; m = 0: b -- one v_bfi_b32 per limb (LLVM makes the AND / OR
+// form two instructions: v_and_b32 + v_and_or_b32)
+__device__ __forceinline__ int32_t bfi(int32_t m, int32_t a, int32_t b) {
+  int32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ fe fsel(int32_t m, const fe& a, const fe& b) {
   fe r;
 #pragma unroll
-  for (int i = 0; i < 10; i++) r.v[i] = (a.v[i] & m) | (b.v[i] & ~m);
+  for (int i = 0; i < 10; i++) r.v[i] = bfi(m, a.v[i], b.v[i]);
   return r;
 }
 __device__ __forceinline__ fe fshl(const fe& f, int32_t sh) {

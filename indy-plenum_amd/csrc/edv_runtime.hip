@@ -496,12 +496,6 @@ int launch_quad(DevCtx& c, DevBuf& qtab, const uint8_t* d_sigs, const uint8_t* d
   HIPOK(launch_quad_kernel(s, va, static_cast<int32_t*>(qtab.p)), "quad launch");
   return 0;
 }
-// A packed block (quad_pack) on the device at d_blob
-int launch_quad_packed(DevCtx& c, DevBuf& qtab, const uint8_t* d_blob, uint64_t n, uint64_t msg_base, uint8_t* d_acc,
-                       hipStream_t s) {
-  return launch_quad(c, qtab, d_blob, d_blob + 64 * n, d_blob + 96 * n + 8 * (n + 1),
-                     reinterpret_cast<const uint64_t*>(d_blob + 96 * n), msg_base, n, d_acc, s);
-}
 
 // Ordinary device path: launch on stream s; caller holds c.mu.  The batch is
 // walked in chunks of c.chunk signatures: [length buckets,] prep kernel, main
@@ -717,6 +711,52 @@ void quad_pack(uint8_t* dst, const uint8_t* sigs, const uint8_t* pks, const uint
             {dst + 96 * n, reinterpret_cast<const uint8_t*>(off + lo), 8 * (n + 1)},
             {dst + 96 * n + 8 * (n + 1), mbytes ? msgs + mbase : nullptr, mbytes}});
   memset(dst + 96 * n + 8 * (n + 1) + mbytes, 0, 64);
+}
+// Device pointers of a latency-path batch
+struct QuadIn {
+  const uint8_t *sigs, *pks, *msgs;
+  const uint64_t* off;
+};
+// Requests [lo, hi) into device buffer `blob` on stream s for the quad kernel.
+// Pinned inputs (the native authenticator's page-locked arena, edv_host_alloc)
+// are DMA'd straight from the caller's memory -- signatures, keys and offsets
+// in one copy when they lie in one host region in that order, then the
+// messages: no host copy on the Node's thread; pageable inputs are packed into
+// the pinned `stage` (quad_pack) and copied in one DMA.
+int quad_upload(DevBuf& blob, PinnedBuf& stage, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
+                const uint64_t* off, uint64_t lo, uint64_t hi, hipStream_t s, QuadIn* d) {
+  const uint64_t n = hi - lo, mbase = off[lo], mbytes = off[hi] - mbase;
+  const uint8_t *src_s = sigs + 64 * lo, *src_p = pks + 32 * lo, *src_m = msgs + mbase;
+  const uint8_t* src_o = reinterpret_cast<const uint8_t*>(off + lo);
+  const bool pinned = is_pinned(src_s) && is_pinned(src_p) && is_pinned(src_o) && (mbytes == 0 || is_pinned(src_m));
+  if (!pinned) {
+    const uint64_t bytes = quad_pack_bytes(n, mbytes);
+    if (stage.ensure(bytes) || blob.ensure(bytes)) return EDV_E_OOM;
+    quad_pack(static_cast<uint8_t*>(stage.p), sigs, pks, msgs, off, lo, hi);
+    HIPOK(hipMemcpyAsync(blob.p, stage.p, bytes, hipMemcpyHostToDevice, s), "h2d packed");
+    uint8_t* b = static_cast<uint8_t*>(blob.p);
+    *d = {b, b + 64 * n, b + 96 * n + 8 * (n + 1), reinterpret_cast<const uint64_t*>(b + 96 * n)};
+    return 0;
+  }
+  const uintptr_t as = reinterpret_cast<uintptr_t>(src_s), ap = reinterpret_cast<uintptr_t>(src_p),
+                  ao = reinterpret_cast<uintptr_t>(src_o);
+  const bool one = ap >= as + 64 * n && ao >= ap + 32 * n && ao + 8 * (n + 1) - as <= 104 * n + 8 + 4096 &&
+                   (ap - as) % 16 == 0 && (ao - as) % 8 == 0;
+  const uint64_t span = one ? ao + 8 * (n + 1) - as : 96 * n + 8 * (n + 1);
+  const uint64_t moff = (span + 15) / 16 * 16;
+  if (blob.ensure(moff + mbytes + 64)) return EDV_E_OOM;
+  uint8_t* b = static_cast<uint8_t*>(blob.p);
+  if (one) {
+    HIPOK(hipMemcpyAsync(b, src_s, span, hipMemcpyHostToDevice, s), "h2d sigs+pks+off");
+    *d = {b, b + (ap - as), b + moff, reinterpret_cast<const uint64_t*>(b + (ao - as))};
+  } else {
+    HIPOK(hipMemcpyAsync(b, src_s, 64 * n, hipMemcpyHostToDevice, s), "h2d sigs");
+    HIPOK(hipMemcpyAsync(b + 64 * n, src_p, 32 * n, hipMemcpyHostToDevice, s), "h2d pks");
+    HIPOK(hipMemcpyAsync(b + 96 * n, src_o, 8 * (n + 1), hipMemcpyHostToDevice, s), "h2d off");
+    *d = {b, b + 64 * n, b + moff, reinterpret_cast<const uint64_t*>(b + 96 * n)};
+  }
+  if (mbytes) HIPOK(hipMemcpyAsync(b + moff, src_m, mbytes, hipMemcpyHostToDevice, s), "h2d msgs");
+  return 0;
 }
 // memcpy of src[0, bounds[K]) into pinned staging over copy_threads() threads,
 // part by part (part k = [bounds[k], bounds[k+1])), with part k's DMA to the
@@ -946,16 +986,15 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
 // into page-locked host memory.  Caller holds c.mu.
 int run_shard_quad(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
                    uint64_t lo, uint64_t hi, uint8_t* accept) {
-  const uint64_t n = hi - lo, mbase = off[lo], bytes = quad_pack_bytes(n, off[hi] - mbase);
+  const uint64_t n = hi - lo, mbase = off[lo];
   const hipStream_t s = c.hs[0];
   if (hipEventQuery(c.st_done) != hipSuccess) {  // the scratch's previous user (any stream)
     (void)hipGetLastError();
     HIPOK(hipStreamWaitEvent(s, c.st_done, 0), "wait scratch");
   }
-  if (c.qstage.ensure(bytes) || c.qblob.ensure(bytes)) return EDV_E_OOM;
-  uint8_t* blob = static_cast<uint8_t*>(c.qstage.p);
-  quad_pack(blob, sigs, pks, msgs, off, lo, hi);
-  HIPOK(hipMemcpyAsync(c.qblob.p, blob, bytes, hipMemcpyHostToDevice, s), "h2d packed");
+  int err;
+  QuadIn d;
+  if ((err = quad_upload(c.qblob, c.qstage, sigs, pks, msgs, off, lo, hi, s, &d))) return err;
   const bool acc_pinned = is_pinned(accept + lo);
   if (!acc_pinned && c.acc_host.ensure(n)) return EDV_E_OOM;
   uint8_t* h_acc = acc_pinned ? accept + lo : static_cast<uint8_t*>(c.acc_host.p);
@@ -966,8 +1005,7 @@ int run_shard_quad(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uin
     if (c.acc.ensure(n)) return EDV_E_OOM;
   }
   uint8_t* d_acc = zc ? static_cast<uint8_t*>(zc) : static_cast<uint8_t*>(c.acc.p);
-  int err;
-  if ((err = launch_quad_packed(c, c.qtab, static_cast<uint8_t*>(c.qblob.p), n, mbase, d_acc, s))) return err;
+  if ((err = launch_quad(c, c.qtab, d.sigs, d.pks, d.msgs, d.off, mbase, n, d_acc, s))) return err;
   if (!zc) HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, s), "d2h accept");
   HIPOK(hipEventRecord(c.st_done, s), "record scratch");
   HIPOK(hipStreamSynchronize(s), "stream sync");
@@ -1143,18 +1181,16 @@ int async_complete(DevCtx& c, DevCtx::AsyncSlot& s) {
 int submit_async_quad(DevCtx& c, DevCtx::AsyncSlot& s, int64_t t, const uint8_t* sigs, const uint8_t* pks,
                       const uint8_t* msgs, const uint64_t* off, uint64_t n, uint8_t* accept, uint8_t* digests,
                       int64_t* ticket) {
-  const uint64_t mbase = off[0], bytes = quad_pack_bytes(n, off[n] - mbase);
+  const uint64_t mbase = off[0];
   if (!s.st) HIPOK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking), "hipStreamCreate");
-  if (s.stage.ensure(bytes) || s.msgs.ensure(bytes) || s.acc.ensure(n) || (digests && s.dig.ensure(32 * n)))
-    return EDV_E_OOM;
+  if (s.acc.ensure(n) || (digests && s.dig.ensure(32 * n))) return EDV_E_OOM;
   s.dig_pinned = digests && is_pinned(digests);
   if (digests && !s.dig_pinned && s.dig_host.ensure(32 * n)) return EDV_E_OOM;
   s.acc_pinned = is_pinned(accept);
   if (!s.acc_pinned && s.acc_host.ensure(n)) return EDV_E_OOM;
-  uint8_t* blob = static_cast<uint8_t*>(s.stage.p);
-  quad_pack(blob, sigs, pks, msgs, off, 0, n);
-  uint8_t* d_blob = static_cast<uint8_t*>(s.msgs.p);
-  HIPOK(hipMemcpyAsync(d_blob, blob, bytes, hipMemcpyHostToDevice, s.st), "h2d packed");
+  int err;
+  QuadIn d;
+  if ((err = quad_upload(s.msgs, s.stage, sigs, pks, msgs, off, 0, n, s.st, &d))) return err;
   uint8_t* h_acc = s.acc_pinned ? accept : static_cast<uint8_t*>(s.acc_host.p);
   void* zc = nullptr;
   if (hipHostGetDevicePointer(&zc, h_acc, 0) != hipSuccess || !zc) {
@@ -1166,15 +1202,13 @@ int submit_async_quad(DevCtx& c, DevCtx::AsyncSlot& s, int64_t t, const uint8_t*
 #ifdef EDV_MEASUREMENT_API
   skip = s.injected = (t == c.inject_fail);
 #endif
-  int err;
-  if (!skip && (err = launch_quad_packed(c, s.qtab, d_blob, n, mbase, d_acc, s.st))) return err;
+  if (!skip && (err = launch_quad(c, s.qtab, d.sigs, d.pks, d.msgs, d.off, mbase, n, d_acc, s.st))) return err;
   if (!zc) HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, s.st), "d2h accept");
   if (digests && !skip) {
     // Request.getDigest of requests whose signing bytes ARE the message (the
     // caller decides which): SHA-256 of the message bytes already on the device
     uint8_t* d_dig = static_cast<uint8_t*>(s.dig.p);
-    if ((err = launch_sha256(d_blob + 96 * n + 8 * (n + 1), reinterpret_cast<const uint64_t*>(d_blob + 96 * n), mbase,
-                             n, d_dig, s.st)))
+    if ((err = launch_sha256(d.msgs, d.off, mbase, n, d_dig, s.st)))
       return err;
     uint8_t* h_dig = s.dig_pinned ? digests : static_cast<uint8_t*>(s.dig_host.p);
     HIPOK(hipMemcpyAsync(h_dig, d_dig, 32 * n, hipMemcpyDeviceToHost, s.st), "d2h digests");

@@ -636,8 +636,10 @@ def test_bench_default_line_contract():
     assert rf["unit"] == "TOP/s" and rf["peak"] > 0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
     ops = rf["ops_per_launch"] / (rf["kernel_ms"] * 1e-3) / 1e12
     assert abs(ops - rf["achieved"]) / rf["achieved"] < 1e-6
-    assert abs(rf["kernel_ms"] - rf["prep_kernel_ms"] - rf["main_kernel_ms"]) < 1e-6
-    assert rf["kernel_ms"] <= line["ms_per_step"] * 1.05
+    assert abs(rf["profile_pair_ms"] - rf["prep_kernel_ms"] - rf["main_kernel_ms"]) < 1e-6
+    # kernel time from HIP events around the timed steps on the library stream
+    assert rf["kernel_ms_source"].startswith("HIP events")
+    assert 0.8 * line["ms_per_step"] <= rf["kernel_ms"] <= line["ms_per_step"] * 1.02
     with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                            "pmc_latest.json")) as f:
         pmc_matches = json.load(f).get("device_code_sha256") == bench.device_code_hash()
