@@ -1,12 +1,12 @@
 // edv_quad.hip -- the latency path: one kernel launch verifies a small batch
-// (a Node's prod, a single Verifier.verify) with FOUR LANES PER SIGNATURE.
+// (a Node's prod, a single Verifier.verify) with EIGHT LANES PER SIGNATURE.
 //
 // The batch path (edv_prep.hip, edv_verify.hip) runs one signature per lane:
 // best for throughput, but a lane's serial chain -- two exponentiations, ~130
 // doublings, ~70 additions, every field product one after the other -- sets
-// the latency of any batch that leaves most of the chip idle (~0.6 ms for
-// n <= 16k: one wave per SIMD at most).  Here a 256-thread workgroup takes 64
-// signatures:
+// the latency of any batch that leaves most of the chip idle (~0.55 ms of
+// kernels for n <= 16k: one wave per SIMD at most).  Here a 256-thread
+// workgroup takes 32 signatures:
 //
 //   phase 1  wave-specialised (uniform within a wave, so no divergence):
 //              wave 0: V2-V4 byte checks, V6/V7 h = SHA-512(R || A || M) mod L,
@@ -15,11 +15,12 @@
 //              wave 2: the same for R
 //              wave 3: [S]B from the shared tables (from identity)
 //            results through LDS, then one barrier;
-//   phase 2  per quad (4 consecutive lanes = one signature): Q = [S]B - R and
-//            the 0..8 x (-A), 0..8 x Q tables, written to global scratch;
-//   phase 3  per quad: the same joint fixed-window walk as the batch path
-//            ([a](-A) + [b](+-Q) == identity), every
-//            point operation split over the quad's lanes.
+//   phase 2  per signature two quads (4 consecutive lanes each): quad 0 builds
+//            the 0..8 x (-A) table, quad 1 computes Q = [S]B - R and builds
+//            0..8 x Q, in global scratch;
+//   phase 3  quad 0 walks [a](-A), quad 1 walks [b](+-Q) -- the batch path's
+//            fixed signed 4-bit windows, split into the
+//            two scalars' walks -- then [a](-A) == -[b](+-Q) projectively.
 //
 // Quad arithmetic.  A point is DISTRIBUTED: lane q of a quad holds coordinate
 // q of (X : Y : Z : T).  The extended-coordinate formulas have four
@@ -28,14 +29,14 @@
 // Z1 T1 | X1 Y1) instead of seven, an addition two instead of eight.  The
 // operands a lane needs are gathered from its quad with DPP quad_perm moves
 // (v_mov_b32_dpp / DPP-modified VOP2 adds: the exchange costs a few VOP2 per
-// limb, no LDS); per-lane signs and selects are mask arithmetic (no VCC-mask
-// v_cndmask_b32, ~23 cycles on gfx950).  A table entry is read one coordinate
-// per lane (48-byte slots): the digit's sign picks which slot (YpX <-> YmX)
-// and negates T2d, so no data is selected after the load.
+// limb, no LDS); per-lane signs and selects are mask arithmetic and v_bfi_b32
+// (no VCC-mask v_cndmask_b32, ~23 cycles on gfx950).  A table entry is read
+// one coordinate per lane (48-byte slots): the digit's sign picks which slot
+// (YpX <-> YmX) and negates T2d, so no data is selected after the load.
 //
 // Same verdicts as the batch path (same strictness checks, same lattice
-// scalars, same walk), checked against libsodium's golden and corpus verdicts
-// by the GPU tests; the field arithmetic is edv_math.h's.
+// scalars, same windows), checked against libsodium's golden and corpus
+// verdicts by the GPU tests; the field arithmetic is edv_math.h's.
 #define EDV_NO_SCHED_FENCE 1
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -46,7 +47,7 @@
 namespace edv {
 namespace {
 
-constexpr int kQSigs = 64;                           // signatures per 256-thread workgroup
+constexpr int kQSigs = 32;                           // signatures per 256-thread workgroup (8 lanes each)
 constexpr int kQCoordWords = 12;                     // one coordinate of a table entry, padded to 48 B
 constexpr int kQEntryWords = 4 * kQCoordWords;       // YpX | YmX | T2d | Z
 constexpr int kQTableWords = kAEntries * kQEntryWords;
@@ -103,6 +104,7 @@ struct QLane {
   int32_t q;           // lane within the quad
   int32_t m1, m2, m3;  // all ones on lane 1 / 2 / 3
   int32_t m01;         // all ones on lanes 0 and 1
+  int32_t m13;         // all ones on lanes 1 and 3
   int32_t s1;          // -1 on lane 1
   int32_t s03, s02;    // -1 on lanes 0, 3 / lanes 0, 2
   int32_t sh2, sh3;    // 1 on lane 2 / lane 3 (shift amounts)
@@ -112,6 +114,7 @@ struct QLane {
     m2 = opaque_i32(-int32_t(q == 2));
     m3 = opaque_i32(-int32_t(q == 3));
     m01 = opaque_i32(-int32_t(q < 2));
+    m13 = opaque_i32(-int32_t(q & 1));
     s1 = m1;
     s03 = opaque_i32(-int32_t(q == 0 || q == 3));
     s02 = opaque_i32(-int32_t(q == 0 || q == 2));
@@ -183,7 +186,7 @@ __device__ __forceinline__ fe slot_load(const int32_t* s) {
 }
 
 // ------------------------------------------------------------ LDS layout
-// per workgroup: phase-1 results for its 64 signatures (structure of arrays:
+// per workgroup: phase-1 results for its 32 signatures (structure of arrays:
 // word w of signature j at [w][j]), and wave 3's [S]B staging slice
 constexpr int kQDigWords = 17;  // da[8] | db[8] | nwin | negR << 8
 constexpr int kQPtWords = 40;   // X | Y | Z | T, 10 limbs each
@@ -220,15 +223,31 @@ __device__ __forceinline__ ge_p3 sb_point(const uint32_t S[8], const int32_t* bt
   return q;
 }
 
-// The latency-path kernel: workgroup g verifies requests base + 64 g .. + 63.
+// A batch of fewer than kQMinLive requests is worked as if it had kQMinLive:
+// the slots past its end repeat its last request (no verdict is written for
+// them).  Measured on MI355X (profiles/r06/quad_sizes_s8.csv): with at most 8
+// live signatures the kernel took 290-360 us on most launches (236 us on one
+// or two of every eight consecutive dispatches), with 12 or more it took
+// 232-240 us on every launch, for the same per-signature work -- an effect of
+// how little of the chip such a launch keeps busy, not of the code path; the
+// padding costs nothing measurable (the extra lanes are idle otherwise).
+constexpr uint64_t kQMinLive = 16;
+
+// The latency-path kernel: workgroup g verifies requests base + 32 g .. + 31,
+// eight lanes per signature from phase 2 on: two quads, h = 0 walking
+// [a](-A) and h = 1 walking [b](+-Q), so each window is four doublings and ONE
+// addition per quad (the joint walk of the batch path adds both entries to one
+// accumulator: two additions in a row), and each quad builds one table.  The
+// verdict is [a](-A) == -[b](+-Q), compared projectively at the end.
 template <int BITS>
 __device__ __forceinline__ void quad_body(const VerifyArgs& a, int32_t* qtab, QuadLds& L) {
   const int tid = int(threadIdx.x), wave = tid >> 6, lane = tid & 63;
   const uint64_t g0 = uint64_t(blockIdx.x) * kQSigs;
-  // ---- phase 1: one role per wave, one signature per lane
-  {
-    const uint64_t j = g0 + uint64_t(lane);
-    const bool in = j < a.n;
+  // ---- phase 1: one role per wave, one signature per lane (lanes 0 .. 31)
+  if (lane < kQSigs) {
+    const uint64_t jl = g0 + uint64_t(lane);
+    const bool in = jl < a.n || jl < kQMinLive;         // worked: a request, or padding of a tiny batch
+    const uint64_t j = jl < a.n ? jl : a.n - 1;           // padding repeats the last request
     const uint64_t i = a.base + (in ? j : 0);
     if (wave == 0) {
       bool ok = false;
@@ -270,88 +289,83 @@ __device__ __forceinline__ void quad_body(const VerifyArgs& a, int32_t* qtab, Qu
     }
   }
   __syncthreads();
-  // ---- phases 2 and 3: one signature per quad
+  // ---- phases 2 and 3: signature js, its quad h
   const QLane Q(lane);
-  const int js = tid >> 2;  // signature within the workgroup
+  const int js = tid >> 3, h = (tid >> 2) & 1;
   const uint64_t j = g0 + uint64_t(js);
-  const bool in = j < a.n;
-  const bool alive = in && L.ok[0][js] && L.ok[1][js] && L.ok[2][js];
-  int32_t* tab = qtab + uint64_t(blockIdx.x * kQSigs + js) * kQSigWords;  // tables of -A (0) and Q (1)
+  const bool in = j < a.n;                              // a verdict to write
+  const bool alive = (in || j < kQMinLive) && L.ok[0][js] && L.ok[1][js] && L.ok[2][js];
+  int32_t* tab = qtab + uint64_t(blockIdx.x * kQSigs + js) * kQSigWords + h * kQTableWords;  // this quad's table
   {
-    // identity entries: YpX = 1, YmX = 1, T2d = 0, Z = 1
+    // identity entry: YpX = 1, YmX = 1, T2d = 0, Z = 1
     fe id = fe_zero();
     id.v[0] = Q.q == 2 ? 0 : 1;
     slot_store(tab + Q.q * kQCoordWords, id);
-    slot_store(tab + kQTableWords + Q.q * kQCoordWords, id);
   }
-  // Q = [S]B - R, then 1..8 x Q; 1..8 x (-A)
-#pragma unroll 1
-  for (int t = 1; t >= 0; t--) {
-    fe p;
-    if (t == 1) p = quad_add(lds_coord(L, 2, js, Q.q), quad_cached(lds_coord(L, 1, js, Q.q), Q), Q);
-    else p = lds_coord(L, 0, js, Q.q);
-    int32_t* tt = tab + t * kQTableWords;
+  // the quad's point: h = 0: -A (plus the identity: the same code in both quads,
+  // no divergence); h = 1: Q = [S]B + (-R); then its table 1..8 x point
+  {
+    fe idc = fe_zero();
+    idc.v[0] = Q.q == 2 ? 0 : 1;
+    const fe cr = quad_cached(lds_coord(L, 1, js, Q.q), Q);  // cached(-R)
+    const int32_t mh = opaque_i32(-int32_t(h));
+    const fe p = quad_add(lds_coord(L, h ? 2 : 0, js, Q.q), fsel(mh, cr, idc), Q);
     const fe e1 = quad_cached(p, Q);
-    slot_store(tt + kQEntryWords + Q.q * kQCoordWords, e1);
+    slot_store(tab + kQEntryWords + Q.q * kQCoordWords, e1);
     fe cur = quad_dbl(p, Q);
 #pragma unroll 1
     for (int e = 2; e < kAEntries; e++) {
       if (e > 2) cur = quad_add(cur, e1, Q);
-      slot_store(tt + e * kQEntryWords + Q.q * kQCoordWords, quad_cached(cur, Q));
+      slot_store(tab + e * kQEntryWords + Q.q * kQCoordWords, quad_cached(cur, Q));
     }
   }
-  // the tables were written by the quad's lanes: make them visible to their
+  // the table was written by the quad's lanes: make it visible to their
   // neighbours (the walk reads the slot its digit's sign selects)
   __syncthreads();
-  // ---- phase 3: the joint walk, window count = the wave's maximum
-  uint32_t da[8], db[8];
+  // ---- phase 3: this quad's walk, window count = the wave's maximum
+  uint32_t d[8];
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    da[k] = L.dig[k][js];
-    db[k] = L.dig[8 + k][js];
-  }
+  for (int k = 0; k < 8; k++) d[k] = L.dig[8 * h + k][js];  // a (h = 0) or |b| (h = 1)
   const uint32_t wf = alive ? L.dig[16][js] : 0u;
   int nwin = int(wf & 0xff);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) nwin = max(nwin, __shfl_xor(nwin, o));
   nwin = __builtin_amdgcn_readfirstlane(nwin);
-  const bool negR = (wf >> 8) & 1;
+  const bool flip = h == 1 && ((wf >> 8) & 1);  // b < 0: the Q walk's digits are negated
   constexpr int kTop = kAWin * (kAWindows - 1);
   constexpr int kTopShl = 32 - kAWin - (kTop - 224);
 #pragma unroll 1
-  for (int k = nwin; k < kAWindows; k++) {
-    shl256<kAWin>(da);
-    shl256<kAWin>(db);
-  }
+  for (int k = nwin; k < kAWindows; k++) shl256<kAWin>(d);
   // identity, distributed: X = 0 | Y = 1 | Z = 1 | T = 0
   fe acc = fe_zero();
   acc.v[0] = (Q.q == 1 || Q.q == 2) ? 1 : 0;
 #pragma unroll 1
   for (int w = nwin - 1; w >= 0; --w) {
-    const int dA = int32_t(da[7] << kTopShl) >> (32 - kAWin);
-    const int dR = int32_t(db[7] << kTopShl) >> (32 - kAWin);
-    shl256<kAWin>(da);
-    shl256<kAWin>(db);
-    // this lane's slot of each entry: YpX and YmX trade places for a negative
+    const int dg = int32_t(d[7] << kTopShl) >> (32 - kAWin);
+    shl256<kAWin>(d);
+    // this lane's slot of the entry: YpX and YmX trade places for a negative
     // digit, and T2d is negated (below)
-    const bool nA = dA < 0, nR = (dR < 0) != negR;
-    const int cA = Q.q < 2 ? (Q.q ^ int(nA)) : Q.q, cR = Q.q < 2 ? (Q.q ^ int(nR)) : Q.q;
-    fe eA = slot_load(tab + (dA < 0 ? -dA : dA) * kQEntryWords + cA * kQCoordWords);
-    fe eR = slot_load(tab + kQTableWords + (dR < 0 ? -dR : dR) * kQEntryWords + cR * kQCoordWords);
+    const bool ng = (dg < 0) != flip;
+    const int c = Q.q < 2 ? (Q.q ^ int(ng)) : Q.q;
+    fe e = slot_load(tab + (dg < 0 ? -dg : dg) * kQEntryWords + c * kQCoordWords);
     if (w != nwin - 1) {
 #pragma unroll 1
-      for (int d = 0; d < kAWin; d++) acc = quad_dbl(acc, Q);
+      for (int k = 0; k < kAWin; k++) acc = quad_dbl(acc, Q);
     }
-    eA = fcneg(eA, opaque_i32(-int32_t(nA && Q.q == 2)));
-    eR = fcneg(eR, opaque_i32(-int32_t(nR && Q.q == 2)));
-    acc = quad_add(acc, eA, Q);
-    acc = quad_add(acc, eR, Q);
+    acc = quad_add(acc, fcneg(e, opaque_i32(-int32_t(ng && Q.q == 2))), Q);
   }
-  // identity: X = 0 (lane 0) and Y - Z = 0 (lane 1)
-  const fe chk = fe_sub(acc, fand(fdpp<qp(0, 2, 2, 2)>(acc), Q.m1));
-  const int32_t z = fe_iszero(chk) ? 1 : 0;
-  const int32_t ok = dpp<qp(0, 0, 0, 0)>(z) & dpp<qp(1, 1, 1, 1)>(z);
-  if (in && Q.q == 0) a.accept[a.base + j] = (alive && ok) ? 1 : 0;
+  // Pa + Pb == identity  <=>  Xa Zb = -Xb Za  and  Ya Zb = Yb Za  (own = this
+  // quad's point, other = the partner quad's, 4 lanes away; symmetric)
+  fe other;
+#pragma unroll
+  for (int i = 0; i < 10; i++) other.v[i] = __shfl_xor(acc.v[i], 4);
+  const fe u = fsel(Q.m13, fdpp<qp(0, 0, 1, 1)>(other), fdpp<qp(0, 0, 1, 1)>(acc));   // Xa | Xb | Ya | Yb
+  const fe v = fsel(Q.m13, fdpp<qp(2, 2, 2, 2)>(acc), fdpp<qp(2, 2, 2, 2)>(other));   // Zb | Za | Zb | Za
+  const fe r = fe_mul(u, v);
+  const fe w2 = fe_add(r, fcneg(fdpp<qp(1, 1, 3, 3)>(r), Q.m2));                      // lane 0: XaZb + XbZa, lane 2: YaZb - YbZa
+  const int32_t z = fe_iszero(w2) ? 1 : 0;
+  const int32_t ok = dpp<qp(0, 0, 0, 0)>(z) & dpp<qp(2, 2, 2, 2)>(z);
+  if (in && h == 0 && Q.q == 0) a.accept[a.base + j] = (alive && ok) ? 1 : 0;
 }
 
 __global__ __launch_bounds__(256) void edv_quad_kernel(VerifyArgs a, int32_t* qtab) {

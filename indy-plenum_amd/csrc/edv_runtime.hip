@@ -712,6 +712,17 @@ void quad_pack(uint8_t* dst, const uint8_t* sigs, const uint8_t* pks, const uint
             {dst + 96 * n + 8 * (n + 1), mbytes ? msgs + mbase : nullptr, mbytes}});
   memset(dst + 96 * n + 8 * (n + 1) + mbytes, 0, 64);
 }
+// Pageable inputs of a latency-path batch are packed into page-locked staging
+// anyway; the quad kernel then reads them from there over PCIe (its phase 1
+// reads each input once, at its start) instead of waiting for a DMA of them:
+// EDV_QUAD_ZERO_COPY=0 turns that off (A/B).
+bool quad_zero_copy() {
+  static const bool on = [] {
+    const char* e = getenv("EDV_QUAD_ZERO_COPY");
+    return !(e && !strcmp(e, "0"));
+  }();
+  return on;
+}
 // Device pointers of a latency-path batch
 struct QuadIn {
   const uint8_t *sigs, *pks, *msgs;
@@ -731,8 +742,16 @@ int quad_upload(DevBuf& blob, PinnedBuf& stage, const uint8_t* sigs, const uint8
   const bool pinned = is_pinned(src_s) && is_pinned(src_p) && is_pinned(src_o) && (mbytes == 0 || is_pinned(src_m));
   if (!pinned) {
     const uint64_t bytes = quad_pack_bytes(n, mbytes);
-    if (stage.ensure(bytes) || blob.ensure(bytes)) return EDV_E_OOM;
+    if (stage.ensure(bytes)) return EDV_E_OOM;
     quad_pack(static_cast<uint8_t*>(stage.p), sigs, pks, msgs, off, lo, hi);
+    void* zc = nullptr;
+    if (quad_zero_copy() && hipHostGetDevicePointer(&zc, stage.p, 0) == hipSuccess && zc) {
+      uint8_t* b = static_cast<uint8_t*>(zc);  // read in place (the staging's previous user is done)
+      *d = {b, b + 64 * n, b + 96 * n + 8 * (n + 1), reinterpret_cast<const uint64_t*>(b + 96 * n)};
+      return 0;
+    }
+    (void)hipGetLastError();
+    if (blob.ensure(bytes)) return EDV_E_OOM;
     HIPOK(hipMemcpyAsync(blob.p, stage.p, bytes, hipMemcpyHostToDevice, s), "h2d packed");
     uint8_t* b = static_cast<uint8_t*>(blob.p);
     *d = {b, b + 64 * n, b + 96 * n + 8 * (n + 1), reinterpret_cast<const uint64_t*>(b + 96 * n)};
