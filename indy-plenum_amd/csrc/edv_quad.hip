@@ -130,7 +130,12 @@ __device__ __forceinline__ fe fe_sq_shift(const fe& f, int32_t sh) {
   int64_t h[10];
   fe_sq_cols<false, false>(f, h);
 #pragma unroll
-  for (int k = 0; k < 10; k++) h[k] = (h[k] << sh) + bias_reg(k);
+  for (int k = 0; k < 10; k++) {
+    // (h << sh) + bias in one v_lshl_add_u64 (its shift may be a VGPR, low 3 bits)
+    int64_t r;
+    asm("v_lshl_add_u64 %0, %1, %2, %3" : "=v"(r) : "v"(h[k]), "v"(sh), "v"(bias_reg(k)));
+    h[k] = r;
+  }
   return fe_carry64_biased(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
 }
 
