@@ -14,6 +14,7 @@
 //                           (SigningSerializer.serialize, toBytes=True)
 //   pack_open_batch         the positional sig||msg split of
 //                           stp_core/crypto/nacl_wrappers.py:232-242 + packing
+//   open_verify             pack_open_batch + the synchronous edv_verify_batch call
 //
 // Any input outside the fast path (non-ASCII base58 text, non-str dict keys,
 // an invalid character, an unacceptable type, ...) returns NotImplemented so the
@@ -355,59 +356,112 @@ PyObject* py_serialize(PyObject*, PyObject* args) {
 // only the items that reach the verifier are packed: crypto_sign_open of
 // sig + msg splits positionally (sm[:64] / sm[64:]), and sm shorter than 64
 // bytes rejects without a verify.  A key that is not 32 bytes -> ValueError.
-PyObject* py_pack_open_batch(PyObject*, PyObject* arg) {
-  PyObject* seq = PySequence_Fast(arg, "pack_open_batch needs a sequence");
-  if (!seq) return nullptr;
-  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+struct OpenPack {
   std::string sigs, pks, msgs;
-  std::vector<uint64_t> off(1, 0);
-  PyObject* idx = PyList_New(0);
-  if (!idx) { Py_DECREF(seq); return nullptr; }
+  std::vector<uint64_t> off{0};
+  std::vector<Py_ssize_t> idx;  // items that reach the verifier
+};
+// 0 = packed, -1 = Python error set
+static int pack_open(PyObject* seq, OpenPack& o) {
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
   for (Py_ssize_t k = 0; k < n; k++) {
     PyObject* it = PySequence_Fast_GET_ITEM(seq, k);
     if (!PyTuple_Check(it) || PyTuple_GET_SIZE(it) != 3) {
       PyErr_SetString(PyExc_TypeError, "items must be (sig, msg, pk) tuples");
-      goto fail;
+      return -1;
     }
-    {
-      char *s, *m, *p;
-      Py_ssize_t ls, lm, lp;
-      if (PyBytes_AsStringAndSize(PyTuple_GET_ITEM(it, 0), &s, &ls) < 0 ||
-          PyBytes_AsStringAndSize(PyTuple_GET_ITEM(it, 1), &m, &lm) < 0 ||
-          PyBytes_AsStringAndSize(PyTuple_GET_ITEM(it, 2), &p, &lp) < 0)
-        goto fail;
-      if (lp != 32) {
-        PyErr_SetString(PyExc_ValueError, "public key must be 32 bytes");
-        goto fail;
-      }
-      if (ls + lm < 64) continue;  // crypto_sign_open: smlen < 64 rejects
-      // sm = sig || msg; signature = sm[:64], message = sm[64:]
-      std::string sm;
-      if (ls == 64) {
-        sigs.append(s, 64);
-        msgs.append(m, size_t(lm));
-      } else {
-        sm.assign(s, size_t(ls));
-        sm.append(m, size_t(lm));
-        sigs.append(sm.data(), 64);
-        msgs.append(sm.data() + 64, sm.size() - 64);
-      }
-      pks.append(p, 32);
-      off.push_back(uint64_t(msgs.size()));
-      PyObject* ki = PyLong_FromSsize_t(k);
-      if (!ki || PyList_Append(idx, ki) < 0) { Py_XDECREF(ki); goto fail; }
-      Py_DECREF(ki);
+    char *s, *m, *p;
+    Py_ssize_t ls, lm, lp;
+    if (PyBytes_AsStringAndSize(PyTuple_GET_ITEM(it, 0), &s, &ls) < 0 ||
+        PyBytes_AsStringAndSize(PyTuple_GET_ITEM(it, 1), &m, &lm) < 0 ||
+        PyBytes_AsStringAndSize(PyTuple_GET_ITEM(it, 2), &p, &lp) < 0)
+      return -1;
+    if (lp != 32) {
+      PyErr_SetString(PyExc_ValueError, "public key must be 32 bytes");
+      return -1;
+    }
+    if (ls + lm < 64) continue;  // crypto_sign_open: smlen < 64 rejects
+    // sm = sig || msg; signature = sm[:64], message = sm[64:]
+    if (ls == 64) {
+      o.sigs.append(s, 64);
+      o.msgs.append(m, size_t(lm));
+    } else {
+      std::string sm(s, size_t(ls));
+      sm.append(m, size_t(lm));
+      o.sigs.append(sm.data(), 64);
+      o.msgs.append(sm.data() + 64, sm.size() - 64);
+    }
+    o.pks.append(p, 32);
+    o.off.push_back(uint64_t(o.msgs.size()));
+    o.idx.push_back(k);
+  }
+  o.msgs.append(64, '\0');  // the kernels read whole words past a message end
+  return 0;
+}
+
+PyObject* py_pack_open_batch(PyObject*, PyObject* arg) {
+  PyObject* seq = PySequence_Fast(arg, "pack_open_batch needs a sequence");
+  if (!seq) return nullptr;
+  OpenPack o;
+  const int r = pack_open(seq, o);
+  Py_DECREF(seq);
+  if (r < 0) return nullptr;
+  PyObject* idx = PyList_New(Py_ssize_t(o.idx.size()));
+  if (!idx) return nullptr;
+  for (size_t i = 0; i < o.idx.size(); i++) {
+    PyObject* ki = PyLong_FromSsize_t(o.idx[i]);
+    if (!ki) { Py_DECREF(idx); return nullptr; }
+    PyList_SET_ITEM(idx, Py_ssize_t(i), ki);
+  }
+  return Py_BuildValue("(y#y#y#y#N)", o.sigs.data(), Py_ssize_t(o.sigs.size()), o.pks.data(),
+                       Py_ssize_t(o.pks.size()), o.msgs.data(), Py_ssize_t(o.msgs.size()),
+                       reinterpret_cast<const char*>(o.off.data()), Py_ssize_t(o.off.size() * 8), idx);
+}
+
+typedef int (*verify_fn_t)(const uint8_t*, const uint8_t*, const uint8_t*, const uint64_t*, uint64_t, uint8_t*,
+                           uint32_t);
+
+// open_verify(items, verify_addr, device_mask) -> list of bools, or the
+// edv_verify_batch error code (an int) for the caller to raise on: pack_open_batch
+// and the synchronous verify in one call, the GIL released around the device
+// call (a Verifier.verify of one request spends no time in numpy or ctypes).
+PyObject* py_open_verify(PyObject*, PyObject* args) {
+  PyObject* items;
+  unsigned long long vaddr;
+  unsigned int mask;
+  if (!PyArg_ParseTuple(args, "OKI", &items, &vaddr, &mask)) return nullptr;
+  const verify_fn_t verify = reinterpret_cast<verify_fn_t>(uintptr_t(vaddr));
+  PyObject* seq = PySequence_Fast(items, "open_verify needs a sequence");
+  if (!seq) return nullptr;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  OpenPack o;
+  const int r = pack_open(seq, o);
+  Py_DECREF(seq);
+  if (r < 0) return nullptr;
+  const size_t nv = o.idx.size();
+  std::vector<uint8_t> acc(nv ? nv : 1, 0);
+  int rc = 0;
+  if (nv) {
+    Py_BEGIN_ALLOW_THREADS
+    rc = verify(reinterpret_cast<const uint8_t*>(o.sigs.data()), reinterpret_cast<const uint8_t*>(o.pks.data()),
+                reinterpret_cast<const uint8_t*>(o.msgs.data()), o.off.data(), uint64_t(nv), acc.data(), mask);
+    Py_END_ALLOW_THREADS
+  }
+  if (rc != 0) return PyLong_FromLong(rc);
+  PyObject* out = PyList_New(n);
+  if (!out) return nullptr;
+  for (Py_ssize_t k = 0; k < n; k++) {
+    Py_INCREF(Py_False);
+    PyList_SET_ITEM(out, k, Py_False);
+  }
+  for (size_t i = 0; i < nv; i++) {
+    if (acc[i]) {
+      Py_DECREF(Py_False);
+      Py_INCREF(Py_True);
+      PyList_SET_ITEM(out, o.idx[i], Py_True);
     }
   }
-  Py_DECREF(seq);
-  msgs.append(64, '\0');  // the kernels read whole words past a message end
-  return Py_BuildValue("(y#y#y#y#N)", sigs.data(), Py_ssize_t(sigs.size()), pks.data(), Py_ssize_t(pks.size()),
-                       msgs.data(), Py_ssize_t(msgs.size()), reinterpret_cast<const char*>(off.data()),
-                       Py_ssize_t(off.size() * 8), idx);
-fail:
-  Py_DECREF(seq);
-  Py_DECREF(idx);
-  return nullptr;
+  return out;
 }
 
 // ------------------------------------------------------ CoreAuthNr fast path
@@ -510,8 +564,6 @@ PyObject* py_prep_core_batch(PyObject*, PyObject* args) {
 // rejected: fast-path requests whose signature did not verify (the caller sets
 // InsufficientCorrectSignatures(0, 1), the replay result of a failed single
 // signature, client_authn.py:110-112).
-typedef int (*verify_fn_t)(const uint8_t*, const uint8_t*, const uint8_t*, const uint64_t*, uint64_t, uint8_t*,
-                           uint32_t);
 typedef int (*host_alloc_t)(uint64_t, void**);
 typedef int (*host_free_t)(void*);
 host_alloc_t g_alloc = nullptr;
@@ -1672,6 +1724,7 @@ PyMethodDef kMethods[] = {
     {"request_digests", py_request_digests, METH_VARARGS,
      "Request.getDigest for a batch: one edv_sha256_batch call at sha_addr (None = use Python)"},
     {"pack_open_batch", py_pack_open_batch, METH_O, "pack (sig, msg, pk) items into the edv C-ABI layout"},
+    {"open_verify", py_open_verify, METH_VARARGS, "crypto_sign_open verdicts of (sig, msg, pk) items, one device call"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_edvhost", "native host prep for the edv verifier", -1, kMethods,

@@ -372,19 +372,16 @@ def open_batch(items, device_mask: int = 0):
     shorter than 64 bytes rejects without reaching the GPU.  pk must be 32 bytes.
     """
     items = list(items)
-    out = [False] * len(items)
     if not items:
-        return out
+        return []
+    addr = verify_address()
     try:
-        sigs, pks, msgs, off, idx = _edvhost.pack_open_batch(items)
+        out = _edvhost.open_verify(items, addr, device_mask)
     except TypeError:  # bytearray / memoryview / list items: normalise, then pack
         items = [(bytes(s), bytes(m), bytes(p)) for s, m, p in items]
-        sigs, pks, msgs, off, idx = _edvhost.pack_open_batch(items)
-    if idx:
-        acc = verify_arrays(np.frombuffer(sigs, np.uint8), np.frombuffer(pks, np.uint8),
-                            np.frombuffer(msgs, np.uint8), np.frombuffer(off, np.uint64), device_mask)
-        for k, ok in zip(idx, acc):
-            out[k] = bool(ok)
+        out = _edvhost.open_verify(items, addr, device_mask)
+    if isinstance(out, int):  # the C-ABI's error code
+        _check(out)
     return out
 
 

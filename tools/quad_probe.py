@@ -20,7 +20,8 @@ def main():
         for _ in range(iters):
             edv.verify_device(b.d_sigs.ptr, b.d_pks.ptr, b.d_msgs.ptr, b.d_off.ptr, n, b.d_accept.ptr, 0,
                               flags=edv.FLAG_UNIFORM_LENGTH)
-        assert b.d_accept.download(n).all()
+        if os.environ.get("QUAD_PROBE_NOCHECK") != "1":  # phase probes write partial verdicts
+            assert b.d_accept.download(n).all()
 
 
 if __name__ == "__main__":
