@@ -434,15 +434,15 @@ def test_golden_on_both_paths(golden, golden_meta, latency_limit, limit):
 
 
 def test_latency_path_batch_sizes_and_entry_points(latency_limit):
-    """Batch sizes around the quad kernel's 64-signature workgroups and its
-    limit, variable message lengths (200..4,096 B) and 20 % damage, through the
+    """Batch sizes around the latency kernel's 32-signature workgroups, its
+    16-slot padding of tiny batches and its limit, variable message lengths (200..4,096 B) and 20 % damage, through the
     synchronous call, the asynchronous one (pageable and page-locked verdicts)
     and the device-resident one with a non-zero msg_base; verdicts equal
     libsodium's (the oracle where it is absent)."""
     latency_limit(8192)
     sigs, pks, msgs, off = orc.corpus(0x1A7, 0, 8192, mode=1, invalid_permille=200)
     want = checker(sigs, pks, msgs, off)
-    for n in (1, 2, 3, 4, 5, 63, 64, 65, 127, 128, 129, 400, 1000, 4095, 4096, 4097, 8192):
+    for n in (1, 2, 3, 4, 5, 15, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 129, 400, 1000, 4095, 4096, 4097, 8192):
         o = off[:n + 1]
         got = edv.verify_arrays(sigs[:64 * n], pks[:32 * n], msgs, o)
         assert np.array_equal(got, want[:n]), n
