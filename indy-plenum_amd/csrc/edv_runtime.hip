@@ -1000,9 +1000,10 @@ int run_shard_fields(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const u
 }
 
 // The latency path of a synchronous call (a shard of at most c.quad_max
-// requests): pack the inputs into the pinned block (a memcpy of a few hundred
-// kB for a Node's prod), one DMA, the quad kernel, verdicts written straight
-// into page-locked host memory.  Caller holds c.mu.
+// requests): inputs DMA'd straight from pinned caller memory, or packed into
+// the pinned staging block and read there by the kernel (quad_upload), the
+// quad kernel, verdicts written straight into page-locked host memory.
+// Caller holds c.mu.
 int run_shard_quad(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint64_t* off,
                    uint64_t lo, uint64_t hi, uint8_t* accept) {
   const uint64_t n = hi - lo, mbase = off[lo];
