@@ -27,6 +27,9 @@ hipError_t launch_sign_kernel(unsigned blocks, hipStream_t s, const uint32_t* se
 // the latency path (edv_quad.hip): requests base .. base + n - 1 of va in one
 // launch, four lanes per signature; qtab: n x kQSigWords words of scratch
 hipError_t launch_quad_kernel(hipStream_t s, const VerifyArgs& va, int32_t* qtab);
+// the right-to-left latency kernel (no table scratch); at most kRtlMax requests
+hipError_t launch_rtl_kernel(hipStream_t s, const VerifyArgs& va);
+constexpr uint64_t kRtlMax = 4096;
 // accept bytes -> bitmask (ceil(n / 8) bytes)
 hipError_t launch_pack_bits_kernel(hipStream_t s, const uint8_t* acc, uint64_t n, uint8_t* bits);
 hipError_t launch_sha256_kernel(unsigned blocks, hipStream_t s, const uint8_t* msgs, const uint64_t* off,

@@ -1,5 +1,8 @@
 // edv_quad.hip -- the latency path: one kernel launch verifies a small batch
-// (a Node's prod, a single Verifier.verify) with EIGHT LANES PER SIGNATURE.
+// (a Node's prod, a single Verifier.verify) with several lanes per signature:
+// edv_rtl_kernel (sixteen lanes, no tables, at most 4,096 requests: below) and
+// edv_quad_kernel (eight lanes, per-signature tables, up to 8,192 requests),
+// described first.
 //
 // The batch path (edv_prep.hip, edv_verify.hip) runs one signature per lane:
 // best for throughput, but a lane's serial chain -- two exponentiations, ~130
@@ -202,7 +205,8 @@ struct QuadLds {
   int32_t stage[kLdsBWaveWords];      // wave 3: LdsBStage slice
 };
 
-__device__ __forceinline__ void lds_put_point(QuadLds& L, int k, int j, const ge_p3& p) {
+template <class Lds>
+__device__ __forceinline__ void lds_put_point(Lds& L, int k, int j, const ge_p3& p) {
 #pragma unroll
   for (int i = 0; i < 10; i++) {
     L.pt[k][i][j] = p.X.v[i];
@@ -211,12 +215,23 @@ __device__ __forceinline__ void lds_put_point(QuadLds& L, int k, int j, const ge
     L.pt[k][30 + i][j] = p.T.v[i];
   }
 }
-// coordinate q of point k of signature j (the quad's distributed form)
-__device__ __forceinline__ fe lds_coord(const QuadLds& L, int k, int j, int q) {
+// coordinate q of a point stored [word][signature] (X | Y | Z | T, 10 limbs
+// each): the quad's distributed form of signature j
+template <int S>
+__device__ __forceinline__ fe coord_get(const int32_t (&pt)[kQPtWords][S], int j, int q) {
   fe f;
 #pragma unroll
-  for (int i = 0; i < 10; i++) f.v[i] = L.pt[k][10 * q + i][j];
+  for (int i = 0; i < 10; i++) f.v[i] = pt[10 * q + i][j];
   return f;
+}
+template <int S>
+__device__ __forceinline__ void coord_put(int32_t (&pt)[kQPtWords][S], int j, int q, const fe& f) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) pt[10 * q + i][j] = f.v[i];
+}
+template <class Lds>
+__device__ __forceinline__ fe lds_coord(const Lds& L, int k, int j, int q) {
+  return coord_get(L.pt[k], j, q);
 }
 
 // [S]B from identity (wave 3 of phase 1)
@@ -238,18 +253,12 @@ __device__ __forceinline__ ge_p3 sb_point(const uint32_t S[8], const int32_t* bt
 // padding costs nothing measurable (the extra lanes are idle otherwise).
 constexpr uint64_t kQMinLive = 16;
 
-// The latency-path kernel: workgroup g verifies requests base + 32 g .. + 31,
-// eight lanes per signature from phase 2 on: two quads, h = 0 walking
-// [a](-A) and h = 1 walking [b](+-Q), so each window is four doublings and ONE
-// addition per quad (the joint walk of the batch path adds both entries to one
-// accumulator: two additions in a row), and each quad builds one table.  The
-// verdict is [a](-A) == -[b](+-Q), compared projectively at the end.
-template <int BITS>
-__device__ __forceinline__ void quad_body(const VerifyArgs& a, int32_t* qtab, QuadLds& L) {
-  const int tid = int(threadIdx.x), wave = tid >> 6, lane = tid & 63;
-  const uint64_t g0 = uint64_t(blockIdx.x) * kQSigs;
-  // ---- phase 1: one role per wave, one signature per lane (lanes 0 .. 31)
-  if (lane < kQSigs) {
+// ---- phase 1 of both latency kernels: one role per wave (uniform, so no
+// divergence), one signature per lane (lanes 0 .. NS - 1); results into L.dig,
+// L.pt and L.ok for the later phases (one barrier after it)
+template <int BITS, int NS, class Lds>
+__device__ __forceinline__ void phase1(const VerifyArgs& a, Lds& L, uint64_t g0, int wave, int lane) {
+  if (lane < NS) {
     const uint64_t jl = g0 + uint64_t(lane);
     const bool in = jl < a.n || jl < kQMinLive;         // worked: a request, or padding of a tiny batch
     const uint64_t j = jl < a.n ? jl : a.n - 1;           // padding repeats the last request
@@ -293,6 +302,19 @@ __device__ __forceinline__ void quad_body(const VerifyArgs& a, int32_t* qtab, Qu
       lds_put_point(L, 2, lane, p);
     }
   }
+}
+
+// The latency-path kernel: workgroup g verifies requests base + 32 g .. + 31,
+// eight lanes per signature from phase 2 on: two quads, h = 0 walking
+// [a](-A) and h = 1 walking [b](+-Q), so each window is four doublings and ONE
+// addition per quad (the joint walk of the batch path adds both entries to one
+// accumulator: two additions in a row), and each quad builds one table.  The
+// verdict is [a](-A) == -[b](+-Q), compared projectively at the end.
+template <int BITS>
+__device__ __forceinline__ void quad_body(const VerifyArgs& a, int32_t* qtab, QuadLds& L) {
+  const int tid = int(threadIdx.x), wave = tid >> 6, lane = tid & 63;
+  const uint64_t g0 = uint64_t(blockIdx.x) * kQSigs;
+  phase1<BITS, kQSigs>(a, L, g0, wave, lane);
   __syncthreads();
   // ---- phases 2 and 3: signature js, its quad h
   const QLane Q(lane);
@@ -373,6 +395,186 @@ __device__ __forceinline__ void quad_body(const VerifyArgs& a, int32_t* qtab, Qu
   if (in && h == 0 && Q.q == 0) a.accept[a.base + j] = (alive && ok) ? 1 : 0;
 }
 
+// ------------------------------------------------ the right-to-left kernel
+// For batches of at most kRtlMax requests: sixteen lanes per signature, four
+// waves with one role each from phase 2 on, and no tables.  [a]P = sum_j d_j
+// 16^j P (signed 4-bit digits from the least significant end): a DOUBLER wave
+// runs the chain P, 16 P, 16^2 P, ... (four distributed doublings per window,
+// the walk's whole serial part, started as soon as phase 1 has P) and
+// publishes each 16^j P in LDS; an ADDER wave adds +-16^j P into bucket |d_j|
+// (bucket 0 takes the zero digits), one cached addition per window, beside the
+// doubler's next four doublings; at the end sum_d d B_d = sum_k T_k with the
+// running sums T_k = B_8 + ... + B_k, the doubler forming T_k while the adder
+// adds up the T's one step behind.  Waves 1 (doubler) and 0 (adder) walk
+// [a](-A), waves 2 and 3 walk [b](+-Q) with Q = [S]B - R; the verdict is
+// [a](-A) == -[b](+-Q), projectively.  The doubler and the adder of a walk
+// meet through two LDS counters, not barriers: the doubler publishes 16^j P
+// into slot j % kRing and then its count (release), the adder waits for the
+// count (acquire), reads the slot and then advances its own count, which the
+// doubler checks before reusing a slot kRing windows later; the adder, with
+// ~half the doubler's work per window, is almost never waited for.  Measured
+// on MI355X (profiles/r06/rtl_kernel.txt): 174-187 us a launch (box to box)
+// against 198-214 us for edv_quad_kernel; the same code with one barrier per
+// window instead of the counters: +10 us.
+constexpr int kRSigs = 16;                 // signatures per 256-thread workgroup
+constexpr int kRing = 4;                   // published points in flight per walk
+struct RtlLds {
+  uint32_t dig[kQDigWords][kRSigs];
+  int32_t pt[3][kQPtWords][kRSigs];        // phase 1: -A, -R, [S]B
+  uint8_t ok[3][kRSigs];
+  int32_t pub[2][kRing][kQPtWords][kRSigs];  // [walk][slot]: the doubler's 16^j P in slot j % kRing (then running sums)
+  int32_t published[2];                    // [walk]: points published so far (the doubler's count)
+  int32_t consumed[2];                     // [walk]: points the adder has read
+  int32_t buckets_done[2];                 // [walk]: the adder's last bucket write is visible
+  int32_t bkt[2][kAEntries][kQPtWords][kRSigs];  // [walk][|digit|]: bucket sums, extended
+  int32_t res[kQPtWords][kRSigs];          // the [b](+-Q) walk's result for the final check
+  int32_t stage[kLdsBWaveWords];           // wave 3 of phase 1: [S]B staging
+  // pads the allocation above half a CU's 160 KiB: one workgroup per CU, so
+  // each role wave has a SIMD of its own (kRtlMax requests fill 256 CUs)
+  int32_t pad[1024];
+};
+static_assert(sizeof(RtlLds) > 80 * 1024, "one workgroup per CU");
+
+__device__ __forceinline__ int lds_acquire(const int32_t* c) {
+  return __hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(int32_t* c, int v) {
+  __hip_atomic_store(c, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// spin (with a short sleep) until *c >= v; every lane of the wave reads the same count
+__device__ __forceinline__ void lds_wait_ge(const int32_t* c, int v) {
+  while (lds_acquire(c) < v) __builtin_amdgcn_s_sleep(1);
+}
+
+__device__ __forceinline__ fe quad_identity(const QLane& L) {
+  fe f = fe_zero();
+  f.v[0] = (L.q == 1 || L.q == 2) ? 1 : 0;  // X = 0 | Y = 1 | Z = 1 | T = 0
+  return f;
+}
+// the cached form of +-P (YpX | YmX | T2d | Z): for -P, YpX and YmX trade
+// places and T2d changes sign
+__device__ __forceinline__ fe quad_cached_signed(const fe& p, int32_t neg, const QLane& L) {
+  const fe c = quad_cached(p, L);
+  const fe sw = fsel(neg & L.m01, fdpp<qp(1, 0, 2, 3)>(c), c);
+  return fcneg(sw, neg & L.m2);
+}
+
+template <int BITS>
+__device__ __forceinline__ void rtl_body(const VerifyArgs& a, RtlLds& L) {
+  const int tid = int(threadIdx.x), wave = tid >> 6, lane = tid & 63;
+  const uint64_t g0 = uint64_t(blockIdx.x) * kRSigs;
+  phase1<BITS, kRSigs>(a, L, g0, wave, lane);
+  __syncthreads();
+  const QLane Q(lane);
+  const int js = lane >> 2;                     // every wave: 16 signatures x 4 lanes
+  const uint64_t j = g0 + uint64_t(js);
+  const bool in = j < a.n;                      // a verdict to write
+  const bool alive = (in || j < kQMinLive) && L.ok[0][js] && L.ok[1][js] && L.ok[2][js];
+  const int walk = (wave == 2 || wave == 3) ? 1 : 0;
+  const bool doubler = wave == 1 || wave == 2;
+  const uint32_t wf = alive ? L.dig[16][js] : 0u;
+  // windows: the workgroup's maximum (all four waves run the same barriers)
+  int nwin = int(wf & 0xff);
+#pragma unroll
+  for (int o = 32; o >= 4; o >>= 1) nwin = max(nwin, __shfl_xor(nwin, o));
+  nwin = __builtin_amdgcn_readfirstlane(nwin);
+  uint32_t d[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) d[k] = alive ? L.dig[8 * walk + k][js] : 0u;  // a, or |b|; dead: all zero
+  const int32_t flip = opaque_i32(-int32_t(walk == 1 && ((wf >> 8) & 1)));  // b < 0: the digits' signs flip
+  fe P;  // the doubler's 16^j P; the adder's sum at the end
+  if (doubler) {
+    if (walk == 0) {
+      P = lds_coord(L, 0, js, Q.q);                                   // -A
+    } else {
+      const fe cr = quad_cached(lds_coord(L, 1, js, Q.q), Q);         // cached(-R)
+      P = quad_add(lds_coord(L, 2, js, Q.q), cr, Q);                  // Q = [S]B - R
+    }
+  } else {
+    const fe id = quad_identity(Q);
+#pragma unroll 1
+    for (int k = 0; k < kAEntries; k++) coord_put(L.bkt[walk][k], js, Q.q, id);
+  }
+  if (tid < 2) {
+    L.published[tid] = 0;
+    L.consumed[tid] = 0;
+    L.buckets_done[tid] = 0;
+  }
+  __syncthreads();
+  if (doubler) {
+#pragma unroll 1
+    for (int w = 0; w < nwin; w++) {
+      if (w > 0) {
+#pragma unroll 1
+        for (int k = 0; k < kAWin; k++) P = quad_dbl(P, Q);
+      }
+      if (w >= kRing) lds_wait_ge(&L.consumed[walk], w - kRing + 1);  // slot w % kRing is free
+      coord_put(L.pub[walk][w % kRing], js, Q.q, P);
+      lds_release(&L.published[walk], w + 1);
+    }
+  } else {
+#pragma unroll 1
+    for (int w = 0; w < nwin; w++) {
+      const int dg = int32_t(d[0] << (32 - kAWin)) >> (32 - kAWin);  // digit w, signed
+      shr256<kAWin>(d);
+      const int32_t ng = opaque_i32(-int32_t(dg < 0)) ^ flip;
+      const int ad = dg < 0 ? -dg : dg;
+      lds_wait_ge(&L.published[walk], w + 1);
+      const fe pw = coord_get(L.pub[walk][w % kRing], js, Q.q);
+      lds_release(&L.consumed[walk], w + 1);  // after the slot's reads (release waits for them)
+      const fe e = quad_cached_signed(pw, ng, Q);
+      coord_put(L.bkt[walk][ad], js, Q.q, quad_add(coord_get(L.bkt[walk][ad], js, Q.q), e, Q));
+    }
+    lds_release(&L.buckets_done[walk], 1);
+  }
+  // sum_d d B_d = sum_k T_k, T_k = B_8 + ... + B_(8 - k): the doubler forms the
+  // T's from the finished buckets and publishes them as points nwin + k; the
+  // adder adds them up as they come (the same two counters)
+  constexpr int kTop = kAEntries - 1;
+  if (doubler) {
+    lds_wait_ge(&L.buckets_done[walk], 1);
+#pragma unroll 1
+    for (int k = 0; k < kTop; k++) {
+      const fe b = coord_get(L.bkt[walk][kTop - k], js, Q.q);
+      P = k == 0 ? b : quad_add(P, quad_cached(b, Q), Q);
+      const int w = nwin + k;
+      lds_wait_ge(&L.consumed[walk], w - kRing + 1);
+      coord_put(L.pub[walk][w % kRing], js, Q.q, P);
+      lds_release(&L.published[walk], w + 1);
+    }
+  } else {
+#pragma unroll 1
+    for (int k = 0; k < kTop; k++) {
+      const int w = nwin + k;
+      lds_wait_ge(&L.published[walk], w + 1);
+      const fe t = coord_get(L.pub[walk][w % kRing], js, Q.q);
+      lds_release(&L.consumed[walk], w + 1);
+      P = k == 0 ? t : quad_add(P, quad_cached(t, Q), Q);
+    }
+  }
+  if (wave == 3) coord_put(L.res, js, Q.q, P);
+  __syncthreads();
+  if (wave != 0) return;
+  // [a](-A) + [b](+-Q) == identity  <=>  Xa Zb = -Xb Za  and  Ya Zb = Yb Za
+  const fe other = coord_get(L.res, js, Q.q);
+  const fe u = fsel(Q.m13, fdpp<qp(0, 0, 1, 1)>(other), fdpp<qp(0, 0, 1, 1)>(P));   // Xa | Xb | Ya | Yb
+  const fe v = fsel(Q.m13, fdpp<qp(2, 2, 2, 2)>(P), fdpp<qp(2, 2, 2, 2)>(other));   // Zb | Za | Zb | Za
+  const fe r = fe_mul(u, v);
+  const fe w2 = fe_add(r, fcneg(fdpp<qp(1, 1, 3, 3)>(r), Q.m2));                     // lane 0: XaZb + XbZa, lane 2: YaZb - YbZa
+  const int32_t z = fe_iszero(w2) ? 1 : 0;
+  const int32_t ok = dpp<qp(0, 0, 0, 0)>(z) & dpp<qp(2, 2, 2, 2)>(z);
+  if (in && Q.q == 0) a.accept[a.base + j] = (alive && ok) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void edv_rtl_kernel(VerifyArgs a) {
+  __shared__ RtlLds lds;
+  rtl_body<kBBits>(a, lds);
+}
+__global__ __launch_bounds__(256) void edv_rtl_kernel_compact(VerifyArgs a) {
+  __shared__ RtlLds lds;
+  rtl_body<kBBitsCompact>(a, lds);
+}
+
 __global__ __launch_bounds__(256) void edv_quad_kernel(VerifyArgs a, int32_t* qtab) {
   __shared__ QuadLds lds;
   quad_body<kBBits>(a, qtab, lds);
@@ -383,6 +585,13 @@ __global__ __launch_bounds__(256) void edv_quad_kernel_compact(VerifyArgs a, int
 }
 
 }  // namespace
+
+hipError_t launch_rtl_kernel(hipStream_t s, const VerifyArgs& va) {
+  const unsigned blocks = unsigned((va.n + kRSigs - 1) / kRSigs);
+  if (va.sb.bits == kBBits) edv_rtl_kernel<<<dim3(blocks), dim3(256), 0, s>>>(va);
+  else edv_rtl_kernel_compact<<<dim3(blocks), dim3(256), 0, s>>>(va);
+  return hipGetLastError();
+}
 
 hipError_t launch_quad_kernel(hipStream_t s, const VerifyArgs& va, int32_t* qtab) {
   const unsigned blocks = unsigned((va.n + kQSigs - 1) / kQSigs);

@@ -476,8 +476,11 @@ bool bucketing_enabled(const DevCtx& c, uint32_t flags) {
 int launch_quad(DevCtx& c, DevBuf& qtab, const uint8_t* d_sigs, const uint8_t* d_pks, const uint8_t* d_msgs,
                 const uint64_t* d_off, uint64_t msg_base, uint64_t n, uint8_t* d_acc, hipStream_t s) {
   if (n == 0) return 0;
+  // up to kRtlMax requests (one workgroup per CU): the right-to-left kernel, no
+  // table scratch; above: the two-walk kernel over per-signature tables
+  const bool rtl = n <= kRtlMax;
   // the last workgroup's 64 quads all write their tables, in range or not
-  if (qtab.ensure((n + 63) / 64 * 64 * kQSigWords * 4)) return EDV_E_OOM;
+  if (!rtl && qtab.ensure((n + 63) / 64 * 64 * kQSigWords * 4)) return EDV_E_OOM;
   VerifyArgs va;
   memset(&va, 0, sizeof va);
   va.sigs = reinterpret_cast<const uint32_t*>(d_sigs);
@@ -493,7 +496,8 @@ int launch_quad(DevCtx& c, DevBuf& qtab, const uint8_t* d_sigs, const uint8_t* d
   HIPOK(hipMemsetAsync(d_acc, 1, n, s), "memset accept");  // measurement build: see launch_main
   return 0;
 #endif
-  HIPOK(launch_quad_kernel(s, va, static_cast<int32_t*>(qtab.p)), "quad launch");
+  if (rtl) HIPOK(launch_rtl_kernel(s, va), "rtl launch");
+  else HIPOK(launch_quad_kernel(s, va, static_cast<int32_t*>(qtab.p)), "quad launch");
   return 0;
 }
 
