@@ -609,10 +609,10 @@ def single_call_leg(calls=200):
         rc.register_authenticator(cpu)
         out["req_authenticator_libsodium_us"] = med_us(lambda: rc.authenticate(req))
         out["verifier_gpu_over_libsodium_time"] = out["verifier_verify_gpu_us"] / out["verifier_verify_libsodium_us"]
-        out["note"] = ("a batch of one takes the latency path (csrc/edv_quad.hip: one launch, eight lanes per "
-                       "signature, ~0.2 ms of kernel bound by its serial chain at one wave per SIMD, "
-                       "profiles/r06/quad_phases.txt); callers verify per prod (INTEGRATION.md way 3), where one "
-                       "call carries hundreds of requests in the same time")
+        out["note"] = ("a batch of one takes the latency path (csrc/edv_quad.hip edv_rtl_kernel: one launch, "
+                       "sixteen lanes per signature, ~0.18 ms of kernel bound by its serial chains at one wave per "
+                       "SIMD, profiles/r06/rtl_kernel.txt); callers verify per prod (INTEGRATION.md way 3), where "
+                       "one call carries hundreds of requests in the same time")
     return out
 
 
