@@ -50,7 +50,8 @@ extern "C" {
  * shard alternates two streams of half-chunk sub-batches, so the copies of
  * one overlap the kernels of the other.  A shard of at most 8,192 requests
  * (a Node's prod, one Verifier.verify) takes the latency path instead
- * (edv_set_latency_path): one kernel launch with eight lanes per signature;
+ * (edv_set_latency_path): one kernel launch with sixteen lanes per signature
+ * (eight above 4,096 requests);
  * pinned inputs are copied by DMA straight from the caller's buffers (one copy
  * when sigs, pks and msg_off lie in one region in that order, then the
  * messages), pageable ones are packed into the library's pinned staging and
@@ -187,13 +188,15 @@ int edv_set_host_slices(int device, int slices);
 
 /* The latency path: every batch of at most max_requests requests (default and
  * at most 8,192; 0 = never) on `device` -- synchronous, asynchronous and
- * device-resident calls alike -- runs as ONE kernel launch with eight lanes per
- * signature (edv_quad.hip: two quads of four lanes, each point doubling and
- * addition split over a quad, operands exchanged by DPP; one quad walks
- * [a](-A), the other [b](+-Q)).  Below one wave per SIMD the batch kernels (one
- * signature per lane) take a lane's whole serial chain whatever n is; this
- * path divides that chain instead (~0.2 ms of kernel on MI355X for 1 to 8,192
- * requests against ~0.55 ms).  Tuning knob: verdicts never depend on it. */
+ * device-resident calls alike -- runs as ONE kernel launch with several lanes
+ * per signature (edv_quad.hip; each point doubling and addition split over a
+ * quad of lanes, operands exchanged by DPP): up to 4,096 requests sixteen lanes
+ * (per scalar a doubler wave running the 16^j P chain and an adder wave
+ * summing per-digit buckets), above that eight (two table walks).  Below one
+ * wave per SIMD the batch kernels (one signature per lane) take a lane's whole
+ * serial chain whatever n is; this path divides that chain instead (0.18-0.21
+ * ms of kernel on MI355X against ~0.55 ms).  Tuning knob: verdicts never
+ * depend on it. */
 int edv_set_latency_path(int device, uint64_t max_requests);
 
 /* SHA-512 length buckets of the device paths (a counting sort of each chunk by
