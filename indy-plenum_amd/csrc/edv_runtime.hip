@@ -57,17 +57,22 @@ struct DevBuf {
 // Pinned (page-locked, portable) host memory: staging of pageable inputs
 struct PinnedBuf {
   void* p = nullptr;
+  void* dev = nullptr;  // its device-side address (zero-copy), looked up once per allocation
   uint64_t cap = 0;
   int ensure(uint64_t bytes) {
     if (bytes <= cap) return 0;
     if (p) (void)hipHostFree(p);
-    p = nullptr; cap = 0;
+    p = nullptr; dev = nullptr; cap = 0;
     bytes = bytes + bytes / 4 + 4096;  // headroom: message bytes vary from call to call
     if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) {
       p = nullptr;
       return set_err(EDV_E_OOM, "hipHostMalloc");
     }
     cap = bytes;
+    if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      dev = nullptr;
+    }
     return 0;
   }
 };
@@ -748,13 +753,11 @@ int quad_upload(DevBuf& blob, PinnedBuf& stage, const uint8_t* sigs, const uint8
     const uint64_t bytes = quad_pack_bytes(n, mbytes);
     if (stage.ensure(bytes)) return EDV_E_OOM;
     quad_pack(static_cast<uint8_t*>(stage.p), sigs, pks, msgs, off, lo, hi);
-    void* zc = nullptr;
-    if (quad_zero_copy() && hipHostGetDevicePointer(&zc, stage.p, 0) == hipSuccess && zc) {
-      uint8_t* b = static_cast<uint8_t*>(zc);  // read in place (the staging's previous user is done)
+    if (quad_zero_copy() && stage.dev) {
+      uint8_t* b = static_cast<uint8_t*>(stage.dev);  // read in place (the staging's previous user is done)
       *d = {b, b + 64 * n, b + 96 * n + 8 * (n + 1), reinterpret_cast<const uint64_t*>(b + 96 * n)};
       return 0;
     }
-    (void)hipGetLastError();
     if (blob.ensure(bytes)) return EDV_E_OOM;
     HIPOK(hipMemcpyAsync(blob.p, stage.p, bytes, hipMemcpyHostToDevice, s), "h2d packed");
     uint8_t* b = static_cast<uint8_t*>(blob.p);
@@ -1012,7 +1015,11 @@ int run_shard_quad(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uin
                    uint64_t lo, uint64_t hi, uint8_t* accept) {
   const uint64_t n = hi - lo, mbase = off[lo];
   const hipStream_t s = c.hs[0];
-  if (hipEventQuery(c.st_done) != hipSuccess) {  // the scratch's previous user (any stream)
+  // the table-free kernel (n <= kRtlMax) touches no device scratch, so it need
+  // not be ordered after (nor before) the scratch's other users; the qblob /
+  // qstage / acc buffers are this call's alone while it holds c.mu
+  const bool scratch = n > kRtlMax;
+  if (scratch && hipEventQuery(c.st_done) != hipSuccess) {  // the scratch's previous user (any stream)
     (void)hipGetLastError();
     HIPOK(hipStreamWaitEvent(s, c.st_done, 0), "wait scratch");
   }
@@ -1022,16 +1029,16 @@ int run_shard_quad(DevCtx& c, const uint8_t* sigs, const uint8_t* pks, const uin
   const bool acc_pinned = is_pinned(accept + lo);
   if (!acc_pinned && c.acc_host.ensure(n)) return EDV_E_OOM;
   uint8_t* h_acc = acc_pinned ? accept + lo : static_cast<uint8_t*>(c.acc_host.p);
-  void* zc = nullptr;
-  if (hipHostGetDevicePointer(&zc, h_acc, 0) != hipSuccess || !zc) {
+  void* zc = acc_pinned ? nullptr : c.acc_host.dev;
+  if (acc_pinned && (hipHostGetDevicePointer(&zc, h_acc, 0) != hipSuccess || !zc)) {
     (void)hipGetLastError();
     zc = nullptr;
-    if (c.acc.ensure(n)) return EDV_E_OOM;
   }
+  if (!zc && c.acc.ensure(n)) return EDV_E_OOM;
   uint8_t* d_acc = zc ? static_cast<uint8_t*>(zc) : static_cast<uint8_t*>(c.acc.p);
   if ((err = launch_quad(c, c.qtab, d.sigs, d.pks, d.msgs, d.off, mbase, n, d_acc, s))) return err;
   if (!zc) HIPOK(hipMemcpyAsync(h_acc, d_acc, n, hipMemcpyDeviceToHost, s), "d2h accept");
-  HIPOK(hipEventRecord(c.st_done, s), "record scratch");
+  if (scratch) HIPOK(hipEventRecord(c.st_done, s), "record scratch");
   HIPOK(hipStreamSynchronize(s), "stream sync");
   if (!acc_pinned) memcpy(accept + lo, h_acc, n);
   return 0;
