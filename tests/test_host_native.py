@@ -711,3 +711,44 @@ def test_failed_async_wait_stays_failed(monkeypatch):
     p2 = sa.authenticate_batch_submit(reqs, digests=False)
     got = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in p2.result()]
     assert got == want
+
+
+def test_open_verify_packs_and_reports_device_errors():
+    """_edvhost.open_verify (edv.open_batch's one native call): the positional
+    sig || msg split of crypto_sign_open before the device call, a list of
+    verdicts with False wherever sm is shorter than 64 bytes, and the C-ABI's
+    error code handed back as an int (edv.open_batch raises on it).  Driven
+    through a C callback standing in for edv_verify_batch (CPU only)."""
+    import ctypes
+    from indy_plenum_amd import _edvhost
+    seen = []
+    VER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32)
+
+    def verify(sigs, pks, msgs, off, n, acc, mask):
+        o = np.ctypeslib.as_array((ctypes.c_uint64 * (n + 1)).from_address(off)).copy()
+        seen.append((ctypes.string_at(sigs, 64 * n), ctypes.string_at(pks, 32 * n),
+                     ctypes.string_at(msgs, int(o[-1])), o.tolist(), mask))
+        ctypes.memmove(acc, bytes([1, 0, 1][:n]) + bytes(max(0, n - 3)), n)
+        return 0
+    cb = VER(verify)
+    addr = ctypes.cast(cb, ctypes.c_void_p).value
+    pk = bytes(range(32))
+    items = [(b"\x01" * 64, b"hello", pk),        # plain: sig 64 B
+             (b"\x02" * 10, b"\x03" * 20, pk),     # sm < 64: rejected without a device call
+             (b"\x04" * 70, b"tail", pk),          # 70-byte "signature": sm[:64], sm[64:]
+             (b"\x05" * 64, b"", pk)]
+    out = _edvhost.open_verify(items, addr, 3)
+    assert out == [True, False, False, True]
+    assert len(seen) == 1
+    sigs, pks, msgs, off, mask = seen[0]
+    assert sigs == b"\x01" * 64 + b"\x04" * 64 + b"\x05" * 64 and pks == pk * 3 and mask == 3
+    assert msgs == b"hello" + b"\x04" * 6 + b"tail" and off == [0, 5, 15, 15]
+    FAIL = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                            ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32)(lambda *a: -3)
+    assert _edvhost.open_verify(items[:1], ctypes.cast(FAIL, ctypes.c_void_p).value, 0) == -3
+    assert _edvhost.open_verify([(b"\x01" * 3, b"", pk)], addr, 0) == [False]   # nothing reaches the device
+    with pytest.raises(ValueError):
+        _edvhost.open_verify([(b"\x01" * 64, b"", b"\x00" * 31)], addr, 0)
+    with pytest.raises(TypeError):
+        _edvhost.open_verify([(bytearray(64), b"", pk)], addr, 0)
