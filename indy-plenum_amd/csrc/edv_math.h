@@ -556,11 +556,15 @@ EDV_HD ge_p3 ge_p3_identity() { return ge_p3{fe_zero(), fe_one(), fe_one(), fe_z
 EDV_HD ge_cached ge_cached_identity() { return ge_cached{fe_one(), fe_one(), fe_one(), fe_zero()}; }
 EDV_HD ge_precomp ge_precomp_identity() { return ge_precomp{fe_one(), fe_one(), fe_zero()}; }
 
+// Operand order: fe_mul(f, g) premultiplies f's odd limbs (x 2, 38 f_9) and
+// g's limbs (x 19), so X and Z go first and Y and T second in every product:
+// each coordinate's premultiplied forms are made once and shared by its two
+// products (the same column sums either way: the product is symmetric).
 EDV_HD ge_p2 ge_p1p1_to_p2(const ge_p1p1& p) {
-  return ge_p2{fe_mul(p.X, p.T), fe_mul(p.Y, p.Z), fe_mul(p.Z, p.T)};
+  return ge_p2{fe_mul(p.X, p.T), fe_mul(p.Z, p.Y), fe_mul(p.Z, p.T)};
 }
 EDV_HD ge_p3 ge_p1p1_to_p3(const ge_p1p1& p) {
-  return ge_p3{fe_mul(p.X, p.T), fe_mul(p.Y, p.Z), fe_mul(p.Z, p.T), fe_mul(p.X, p.Y)};
+  return ge_p3{fe_mul(p.X, p.T), fe_mul(p.Z, p.Y), fe_mul(p.Z, p.T), fe_mul(p.X, p.Y)};
 }
 EDV_HD ge_p2 ge_p3_to_p2(const ge_p3& p) { return ge_p2{p.X, p.Y, p.Z}; }
 EDV_HD ge_cached ge_p3_to_cached(const ge_p3& p) {
