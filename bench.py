@@ -882,7 +882,9 @@ def c5_leg(n=20000, n_cpu=2000):
                       "gpu_vs_same_path_verify_skipped": out.get("overlap_vs_verify_skipped"),
                       "verify_skipped_ordered_req_per_s": out.get("gpu_overlap_verify_skipped", {}).get(
                           "ordered_req_per_s_one_process"),
-                      "gpu_mode": "overlap: authenticate_batch_submit per prod, handed over at the next prod",
+                      "gpu_mode": ("overlap: authenticate_batch_submit per prod, handed over at the end of the same prod when "
+                                   "the GPU is done by then (PendingProd.ready), else at the next prod"),
+                      "early_handovers": out.get("gpu_batched_overlap", {}).get("early_handovers"),
                       "cpu_ordered_req_per_s": out.get("cpu_reference", {}).get("ordered_req_per_s_one_process"),
                       "cpu_auth_share_of_node_time": out.get("cpu_reference", {}).get("auth_share_of_node_time")}
     return out

@@ -95,6 +95,12 @@ int edv_verify_batch_async(const uint8_t *sigs, const uint8_t *pks, const uint8_
  * failed, every wait for a ticket at or below it that is no longer pending
  * returns EDV_E_HIP, however many batches fail later. */
 int edv_wait_async(int device, int64_t ticket);
+/* edv_wait_async without the wait: EDV_PENDING while batch `ticket` of `device`
+ * is still on the GPU (nothing changes), else exactly what edv_wait_async
+ * returns, with the verdicts handed over.  Lets a Node hand a prod's batch over
+ * in the same prod when the GPU is already done, and at its next prod if not. */
+#define EDV_PENDING 1
+int edv_query_async(int device, int64_t ticket);
 /*
  * edv_verify_batch_async that also returns, when `digests` is not NULL, the
  * SHA-256 of every message (digests: n x 32 bytes, same lifetime rules as

@@ -65,17 +65,23 @@ class PendingAuth:
     digests() -> per request the Request.getDigest hex string or None.  The
     first call waits; both may be called any number of times."""
 
-    __slots__ = ("_finish", "_res")
+    __slots__ = ("_finish", "_res", "_ready")
 
-    def __init__(self, finish):
+    def __init__(self, finish, ready=None):
         self._finish = finish
         self._res = None
+        self._ready = ready  # () -> bool: the device is done (None: the work was done at submission)
 
     def _get(self):
         if self._res is None:
             self._res = self._finish()
-            self._finish = None
+            self._finish = self._ready = None
         return self._res
+
+    def ready(self):
+        """True when result() will not wait for the GPU (it may still build the
+        per-request results); False while the batch is on the device."""
+        return self._res is not None or self._ready is None or self._ready()
 
     def result(self):
         return self._get()[0]
@@ -407,7 +413,8 @@ class CoreAuthMixin:
             h = _edvhost.auth_core_submit(reqs, self.clients, self.excluded_from_signing, submit, wait,
                                           edv.batch_device(), edv.PREP_THREADS, self._state_nyms(reqs),
                                           digests and self.device_digests_ok())
-            return PendingAuth(lambda: self._finish_native(reqs, h, verifier))
+            return PendingAuth(lambda: self._finish_native(reqs, h, verifier),
+                               lambda: _edvhost.batch_ready(h, edv.query_address()))
         out = self.authenticate_batch(reqs, verifier)
         return PendingAuth(lambda: (out, [None] * len(reqs)))
 

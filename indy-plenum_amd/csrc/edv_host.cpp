@@ -1172,6 +1172,31 @@ PyObject* py_auth_core_finish(PyObject*, PyObject* cap) {
   return r4;
 }
 
+// batch_ready(handle, query_addr) -> bool for an auth_core_submit or
+// req_auth_submit handle: True when its finish will not wait for the device
+// (the batch is done and its verdicts are in the arena, it failed -- finish
+// raises -- or nothing was submitted), False while it is still on the GPU.
+// query_addr: edv_query_async (EDV_PENDING = 1 while running).  Lets the Node
+// hand a prod's batch over in the same prod when the GPU is already done.
+typedef int (*query_fn_t)(int, int64_t);
+PyObject* py_batch_ready(PyObject*, PyObject* args) {
+  PyObject* cap;
+  unsigned long long qaddr;
+  if (!PyArg_ParseTuple(args, "OK", &cap, &qaddr)) return nullptr;
+  Batch* b = static_cast<Batch*>(PyCapsule_GetPointer(cap, kBatchCapsule));
+  if (!b) return nullptr;
+  if (!b->pending || b->failed) Py_RETURN_TRUE;
+  const query_fn_t query = reinterpret_cast<query_fn_t>(uintptr_t(qaddr));
+  int rc;
+  Py_BEGIN_ALLOW_THREADS  // the query takes the device's lock, which a synchronous call may hold
+  rc = query(b->device, b->ticket);
+  Py_END_ALLOW_THREADS
+  if (rc == 1) Py_RETURN_FALSE;
+  b->pending = false;
+  if (rc != 0) b->failed = true;  // the finish raises, as after a failed wait (the arena is not reused)
+  Py_RETURN_TRUE;
+}
+
 // ---- ReqAuthenticator.authenticate_batch_submit for the single stock
 // CoreAuthNr (req_authenticator.py:22-44 per request): the txn-type routing too.
 // req_auth_submit(reqs, clients, excluded, submit_addr, wait_addr, device, threads,
@@ -1715,6 +1740,8 @@ PyMethodDef kMethods[] = {
      "wait for a req_auth_submit handle: (out, slow, general, digests or None)"},
     {"auth_core_finish", py_auth_core_finish, METH_O,
      "wait for an auth_core_submit handle: (out, slow, rejected, digests or None)"},
+    {"batch_ready", py_batch_ready, METH_VARARGS,
+     "True when finishing a submitted handle will not wait for the device (edv_query_async at query_addr)"},
     {"set_host_allocator", py_set_host_allocator, METH_VARARGS,
      "page-locked arena allocator (edv_host_alloc, edv_host_free addresses)"},
     {"prep_core_batch", py_prep_core_batch, METH_VARARGS, "CoreAuthNr single-signature fast path (None = Python)"},

@@ -1688,6 +1688,28 @@ int edv_wait_async(int device, int64_t ticket) {
   return 0;
 }
 
+int edv_query_async(int device, int64_t ticket) {
+  g_err.clear();
+  CtxLock cl(device);
+  if (cl.err) return cl.err;
+  if (!cl.c->ledger.known(ticket)) return set_err(EDV_E_ARG, "unknown ticket");
+  for (auto& s : cl.c->as) {
+    if (s.ticket != ticket) continue;
+    const hipError_t e = hipEventQuery(s.done);
+    if (e == hipErrorNotReady) {
+      (void)hipGetLastError();
+      return EDV_PENDING;
+    }
+    if (e != hipSuccess) {
+      async_fail(*cl.c, s);
+      return set_err(EDV_E_HIP, "async query", e);
+    }
+    return async_complete(*cl.c, s);  // done: hand over as edv_wait_async would, without blocking
+  }
+  if (cl.c->ledger.settled(ticket) != 0) return set_err(EDV_E_HIP, "async batch failed earlier");
+  return 0;
+}
+
 int edv_sha256_batch(const uint8_t* msgs, const uint64_t* msg_off, uint64_t n, uint8_t* out, uint32_t device_mask) {
   g_err.clear();
   if (n == 0) return 0;

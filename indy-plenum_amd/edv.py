@@ -94,6 +94,8 @@ def lib():
         h.edv_verify_digest_batch_async.restype = ctypes.c_int
         h.edv_wait_async.argtypes = [ctypes.c_int, ctypes.c_int64]
         h.edv_wait_async.restype = ctypes.c_int
+        h.edv_query_async.argtypes = [ctypes.c_int, ctypes.c_int64]
+        h.edv_query_async.restype = ctypes.c_int
         h.edv_pipeline_sync.argtypes = [ctypes.c_int]
         h.edv_pipeline_sync.restype = ctypes.c_int
         h.edv_sign_batch_dev.argtypes = [vp, vp, vp, u64, u64, vp, vp, ctypes.c_int, vp]
@@ -312,6 +314,20 @@ def wait_async(ticket: int, device: int = 0) -> None:
     _check(lib().edv_wait_async(device, ticket))
 
 
+EDV_PENDING = 1
+
+
+def query_async(ticket: int, device: int = 0) -> bool:
+    """wait_async without the wait: False while batch `ticket` is still on the
+    GPU, True once it is done (its verdicts then handed over, as wait_async
+    would); raises as wait_async would for a failed batch."""
+    rc = lib().edv_query_async(device, ticket)
+    if rc == EDV_PENDING:
+        return False
+    _check(rc)
+    return True
+
+
 def sha256_arrays(msgs, offsets, device_mask: int = 0) -> np.ndarray:
     """SHA-256 of n messages in the C-ABI layout -> (n, 32) uint8 digests (row f-3)."""
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -418,6 +434,17 @@ def async_addresses():
         _async_addrs = (ctypes.cast(h.edv_verify_digest_batch_async, ctypes.c_void_p).value,
                         ctypes.cast(h.edv_wait_async, ctypes.c_void_p).value)
     return _async_addrs
+
+
+_query_addr = None
+
+
+def query_address() -> int:
+    """Address of edv_query_async (the native batch handles' ready() calls it)."""
+    global _query_addr
+    if _query_addr is None:
+        _query_addr = ctypes.cast(lib().edv_query_async, ctypes.c_void_p).value
+    return _query_addr
 
 
 BATCH_DEVICE = None            # device of the native asynchronous whole-batch path (None: batch_device())

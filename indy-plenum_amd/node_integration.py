@@ -91,13 +91,19 @@ def authenticate_prod(authenticator: ReqAuthenticator, client_msgs: Sequence[Tup
 class PendingProd:
     """One prod's REQUESTs and PROPAGATEs submitted for authentication (and
     their request digests) without waiting: finish() hands each message its
-    outcome in arrival order, as authenticate_prod does, one prod later."""
+    outcome in arrival order, as authenticate_prod does -- at the end of the
+    same prod if ready() says the GPU is already done, else one prod later."""
 
     def __init__(self, authenticator: ReqAuthenticator, client_msgs, propagates, digests: bool = True):
         self.client_msgs, self.propagates = list(client_msgs), list(propagates)
         self.t_read = 0.0  # when the messages were read (the caller's clock), for latency bookkeeping
         self.reqs = [m["request"] for m, _frm in self.propagates] + [m for m, _frm in self.client_msgs]
         self._pending = authenticator.authenticate_batch_submit(self.reqs, digests=digests) if self.reqs else None
+
+    def ready(self):
+        """True when finish() will not wait for the GPU: the Node may then hand
+        the prod over at once instead of at its next prod."""
+        return self._pending is None or self._pending.ready()
 
     def digests(self, digest_fn=None):
         """Request.getDigest of every request (propagates first): the device's,

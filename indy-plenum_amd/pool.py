@@ -36,10 +36,13 @@ one-message-at-a-time verifySignature.  Request keys are Request.getDigest
 
 `overlap=True` (batched only) submits a prod's authentication batch without
 waiting (ReqAuthenticator.authenticate_batch_submit: host prep now, one queued
-device call that also hashes the request digests) and handles its verdicts at
-the node's next prod, so the GPU round trip of one node's batch runs while the
-nodes do their Python work.  Each message is still handled exactly once with
-its own verdict, in arrival order; it is only handled one prod later.
+device call that also hashes the request digests) and handles its verdicts
+later, so the GPU round trip of one node's batch runs while the node does its
+Python work: with handover="early" (default) at the end of the same prod if
+the GPU is done by then (PendingProd.ready, a non-blocking edv_query_async),
+else at the node's next prod; with handover="next" always at the next prod.
+Each message is still handled exactly once with its own verdict, in arrival
+order.
 """
 import gc
 import hashlib
@@ -135,10 +138,17 @@ class _TimedAuth:
 class PoolNode:
     def __init__(self, name, peers, authenticator, f, batched=True, digest_fn=cpu_digests,
                  client_quota=DEFAULT_LISTENER_QUOTA, node_quota=DEFAULT_LISTENER_QUOTA, max_batch=1000,
-                 overlap=False):
+                 overlap=False, handover="early"):
         self.name, self.peers, self.f = name, list(peers), f
         self.overlap = overlap and batched
-        self._pending = None          # PendingProd of the previous prod (overlap mode)
+        if handover not in ("early", "next"):
+            raise ValueError("handover must be 'early' or 'next'")
+        # overlap mode: "early" hands a prod's batch over at the end of the same
+        # prod when the GPU is already done (PendingProd.ready), else at the next
+        # prod; "next" always at the next prod
+        self.early = handover == "early"
+        self.early_handovers = 0
+        self._pending = None          # PendingProd not yet handed over (overlap mode)
         self.auth = _TimedAuth(authenticator, self)
         self.n = len(self.peers) + 1
         self.batched, self.digest_fn = batched, digest_fn
@@ -217,6 +227,13 @@ class PoolNode:
         n_work = len(props) + len(clients) + len(three_pc) + (self._pending is not None)
         for m, frm in three_pc:
             getattr(self, "_on_" + m["op"])(m, frm)
+        if self.early and self._pending is not None:
+            with _AuthWindow(self):
+                done = self._pending.ready()
+            if done:  # this prod's batch is verified already: hand it over now
+                pend, self._pending = self._pending, None
+                self.early_handovers += 1
+                self._finish(pend)
         self._service_replica()
         self.flush(pool)
         self.busy_s += time.perf_counter() - t0
@@ -446,6 +463,7 @@ class Pool:
         return {"ordered_per_node": [nd.ordered for nd in nodes], "nacks_per_node": [nd.nacks for nd in nodes],
                 "bad_propagates": sum(nd.bad_propagates for nd in nodes),
                 "verifies": sum(nd.verifies for nd in nodes), "auth_calls": sum(nd.auth_calls for nd in nodes),
+                "early_handovers": sum(nd.early_handovers for nd in nodes),
                 "wall_s": wall_s, "ordered_req_per_s_one_process": n_reqs / wall_s,
                 "max_node_busy_s": busy, "ordered_req_per_s_parallel_nodes": n_reqs / busy,
                 "auth_share_of_node_time": auth / node,

@@ -159,7 +159,7 @@ class ReqAuthenticator:
             for k, d in zip(todo, p.digests()):
                 dig[k] = d
             return out, dig
-        return PendingAuth(finish)
+        return PendingAuth(finish, p.ready if hasattr(p, "ready") else (lambda: False))
 
     def _native_submit(self, reqs, digests):
         """The whole submission natively (_edvhost.req_auth_submit: the type
@@ -196,7 +196,7 @@ class ReqAuthenticator:
                     for k, r in zip(general, self._authenticate_batch([reqs[k] for k in general])):
                         out[k] = r
             return out, (digs if digs is not None else [None] * len(reqs))
-        return PendingAuth(finish)
+        return PendingAuth(finish, lambda: _edvhost.batch_ready(h, edv.query_address()))
 
     def _authenticate_batch(self, reqs):
         fast = self._single_stock(reqs)

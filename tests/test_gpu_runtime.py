@@ -795,6 +795,63 @@ def test_async_failure_end_to_end_with_fault_hook():
     pin.free()
 
 
+def test_query_async_hands_over_without_waiting():
+    """edv_query_async (the Node's early hand-over, pool.py handover="early"):
+    EDV_PENDING while a batch runs, then 0 with the verdicts in the caller's
+    buffer -- latency-path and batch-path sizes, pageable and page-locked
+    verdicts -- and 0 again when asked twice; EDV_E_ARG for a ticket never
+    issued; a failed batch (fault hook of the measurement build) answers
+    EDV_E_HIP with all-zero verdicts, and the wait after it says the same."""
+    import ctypes
+    import time
+    lib = edv.lib()
+    dev = 0
+    cases = [orc.corpus(0x9E40 + k, 0, n, mode=k % 2, invalid_permille=80) for k, n in enumerate((400, 65536))]
+    wants = [checker(*c) for c in cases]
+    pin = edv.PinnedBuffer(65536 + 64)
+
+    def poll(query, t, limit_s=20.0):
+        t0 = time.time()
+        while True:
+            rc = query(dev, t)
+            if rc != edv.EDV_PENDING:
+                return rc
+            assert time.time() - t0 < limit_s, "batch never completed"
+            time.sleep(0.0001)
+
+    for pinned in (False, True):
+        for (sigs, pks, msgs, off), want in zip(cases, wants):
+            n = len(off) - 1
+            acc = pin.array[:n] if pinned else np.full(n, 7, np.uint8)
+            acc[:] = 7
+            t = ctypes.c_int64(-1)
+            assert lib.edv_verify_batch_async(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, off.ctypes.data,
+                                              n, acc.ctypes.data, dev, ctypes.byref(t)) == 0
+            assert poll(lib.edv_query_async, t.value) == 0
+            assert np.array_equal(acc, want), (pinned, n)
+            assert lib.edv_query_async(dev, t.value) == 0 and lib.edv_wait_async(dev, t.value) == 0
+            assert edv.query_async(t.value, dev)
+    assert lib.edv_query_async(dev, t.value + 1000) == edv.EDV_E_ARG
+    pin.free()
+    # a failed batch, through the measurement build's fault hook
+    ml = edv.measure_lib()
+    ml.edv_query_async.argtypes = [ctypes.c_int, ctypes.c_int64]
+    sigs, pks, msgs, off = cases[0]
+    n = len(off) - 1
+    acc = np.full(n, 7, np.uint8)
+    t = ctypes.c_int64(-1)
+    assert ml.edv_verify_batch_async(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, off.ctypes.data, n,
+                                     acc.ctypes.data, dev, ctypes.byref(t)) == 0
+    assert poll(ml.edv_query_async, t.value) == 0
+    assert ml.edv_test_fail_async(dev, t.value + 1) == 0
+    assert ml.edv_verify_batch_async(sigs.ctypes.data, pks.ctypes.data, msgs.ctypes.data, off.ctypes.data, n,
+                                     acc.ctypes.data, dev, ctypes.byref(t)) == 0
+    assert poll(ml.edv_query_async, t.value) == edv.EDV_E_HIP
+    assert not acc.any()
+    assert ml.edv_wait_async(dev, t.value) == edv.EDV_E_HIP
+    assert ml.edv_test_fail_async(dev, -1) == 0
+
+
 def test_context_memory_and_table_sets():
     """edv_context_memory reports the library's device
     memory by kind.  In a fresh process with the default table policy a

@@ -428,8 +428,20 @@ def _oracle_async_callbacks(calls):
             return -1
         issued[ticket] = True
         return 0
-    cbs = (SUB(submit), WAIT(wait))
-    return cbs, tuple(ctypes.cast(c, ctypes.c_void_p).value for c in cbs), issued
+
+    def query(device, ticket):  # edv_query_async: done at submit, so handed over now
+        if not 0 <= ticket < len(issued):
+            return -1
+        issued[ticket] = True
+        return 0
+    cbs = (SUB(submit), WAIT(wait), WAIT(query))
+    return cbs, tuple(ctypes.cast(c, ctypes.c_void_p).value for c in cbs[:2]), issued
+
+
+def _query_address(cbs):
+    """edv.query_address stand-in for _oracle_async_callbacks' query callback."""
+    import ctypes
+    return lambda: ctypes.cast(cbs[2], ctypes.c_void_p).value
 
 
 @pytest.mark.parametrize("with_state", [False, True])
@@ -711,6 +723,78 @@ def test_failed_async_wait_stays_failed(monkeypatch):
     p2 = sa.authenticate_batch_submit(reqs, digests=False)
     got = [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x) for x in p2.result()]
     assert got == want
+
+
+def test_batch_ready_queries_without_waiting(monkeypatch):
+    """PendingAuth.ready() / PendingProd.ready() through _edvhost.batch_ready and
+    an edv_query_async-compatible callback: False while the query answers
+    EDV_PENDING (and no wait happens), True once it answers 0 -- after which
+    result() hands the verdicts over without calling the wait at all, with the
+    same results as the sequential chain; a failed query makes ready() True and
+    result() raise, for good.  Both submit paths (CoreAuthNr and the native
+    ReqAuthenticator one) carry it."""
+    import ctypes
+    import test_authn_host as H
+    from indy_plenum_amd import client_authn
+    from indy_plenum_amd.node_integration import PendingProd
+    from indy_plenum_amd.req_authenticator import ReqAuthenticator
+    sa, reqs = H.make_requests(400, seed=93)
+    with monkeypatch.context() as m:
+        m.setattr(edv, "open_batch", H.oracle_open_batch)
+        want = [H.outcome(lambda q=q: sa.authenticate(q)) for q in reqs]
+    calls = []
+    cbs, addrs, issued = _oracle_async_callbacks(calls)
+    QUERY = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.c_int64)
+    state = {"answer": 1, "queries": 0}
+
+    def query(device, ticket):
+        state["queries"] += 1
+        if state["answer"] == 0:
+            issued[ticket] = True       # handed over by the query, as edv_query_async does
+        return state["answer"]
+    qf = QUERY(query)
+    monkeypatch.setattr(edv, "async_addresses", lambda: addrs)
+    monkeypatch.setattr(edv, "query_address", lambda: ctypes.cast(qf, ctypes.c_void_p).value)
+    monkeypatch.setattr(edv, "BATCH_DEVICE", 0)
+    monkeypatch.setattr(edv, "verify_address", lambda: addrs[0])
+    monkeypatch.setattr(client_authn.CoreAuthMixin, "STATE_KEYS_ON_DEVICE", 10**9)
+    monkeypatch.setattr(edv, "_OPEN_BATCH", H.oracle_open_batch)
+    monkeypatch.setattr(edv, "open_batch", H.oracle_open_batch)
+    norm = lambda res: [("raise", type(x).__name__, x.args) if isinstance(x, BaseException) else ("ok", x)
+                        for x in res]
+    ra = ReqAuthenticator()
+    ra.register_authenticator(sa)
+    with monkeypatch.context() as m:
+        m.setattr(edv, "open_batch", H.oracle_open_batch)
+        want_ra = [H.outcome(lambda q=q: ra.authenticate(q)) for q in reqs]
+    for submit, expect in ((lambda: sa.authenticate_batch_submit(reqs, digests=True), want),
+                           (lambda: ra.authenticate_batch_submit(reqs, digests=True), want_ra)):
+        state.update(answer=1, queries=0)
+        p = submit()
+        t = len(issued) - 1
+        assert not p.ready() and not p.ready() and state["queries"] == 2 and issued[t] is False
+        state["answer"] = 0
+        assert p.ready() and issued[t] is True
+        assert p.ready() and state["queries"] == 3        # settled: no further query
+        assert norm(p.result()) == expect                 # the wait callback was not called again
+    # PendingProd: ready() follows the batch
+    good = [q for q in reqs if isinstance(q, dict) and q.get("identifier")]
+    state.update(answer=1, queries=0)
+    pp = PendingProd(ra, [(q, "client") for q in good], [], digests=True)
+    assert not pp.ready()
+    state["answer"] = 0
+    assert pp.ready()
+    seen = []
+    pp.finish(lambda m, f, o: seen.append(o), lambda m, f, o: seen.append(o))
+    assert len(seen) == len(good)
+    assert PendingProd(ra, [], []).ready()                # nothing submitted
+    # a failed query: ready, and the result raises every time
+    state.update(answer=-3)
+    p = sa.authenticate_batch_submit(reqs, digests=False)
+    assert p.ready()
+    for _ in range(2):
+        with pytest.raises(RuntimeError, match="failed earlier"):
+            p.result()
 
 
 def test_open_verify_packs_and_reports_device_errors():

@@ -115,21 +115,25 @@ def test_pool_run_ending_with_batches_in_flight(monkeypatch):
     assert st["verifies"] == 4 * len(reqs) + 4 * 3 * len(valid)
 
 
-def test_pool_overlap_on_the_native_async_path(monkeypatch):
+@pytest.mark.parametrize("handover", ["early", "next"])
+def test_pool_overlap_on_the_native_async_path(monkeypatch, handover):
     """overlap=True through the real native asynchronous path (auth_core_submit /
     auth_core_finish, device digests) with the device calls answered by the
-    oracle and hashlib: the same ordered set and NACKs as the reference flow."""
-    from test_host_native import _oracle_async_callbacks
+    oracle and hashlib: the same ordered set and NACKs as the reference flow,
+    whether a prod's batch is handed over at the end of the same prod (the
+    stand-in is done at once, so every prod that submits does) or at the next."""
+    from test_host_native import _oracle_async_callbacks, _query_address
     calls = []
     cbs, addrs, issued = _oracle_async_callbacks(calls)
     monkeypatch.setattr(edv, "async_addresses", lambda: addrs)
+    monkeypatch.setattr(edv, "query_address", _query_address(cbs))
     monkeypatch.setattr(edv, "BATCH_DEVICE", 0)
     monkeypatch.setattr(edv, "verify_address", lambda: addrs[0])
     monkeypatch.setattr(edv, "_OPEN_BATCH", H.oracle_open_batch)
     monkeypatch.setattr(edv, "open_batch", H.oracle_open_batch)
     signers, reqs, valid = flood()
     pool = Pool(factory(signers), n=4, batched=True, digest_fn=cpu_digests, overlap=True, client_quota=16,
-                max_batch=7)
+                max_batch=7, handover=handover)
     pool.submit(reqs)
     try:
         wall = pool.run(len(valid))
@@ -141,7 +145,11 @@ def test_pool_overlap_on_the_native_async_path(monkeypatch):
     keys = [nd.ordered_keys for nd in pool.nodes.values()]
     assert all(k == keys[0] for k in keys) and keys[0] == set(cpu_digests(valid))
     assert calls and all(d for _n, d in calls)          # every batch asked for device digests
-    assert all(issued)                                  # every queued batch was waited for
+    assert all(issued)                                  # every queued batch was handed over
+    if handover == "early":
+        assert st["early_handovers"] == st["auth_calls"]
+    else:
+        assert st["early_handovers"] == 0
 
 
 @pytest.mark.parametrize("batched,overlap", [(False, False), (True, True)])

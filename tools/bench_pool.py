@@ -76,10 +76,10 @@ def factory(clients, cls):
     return make
 
 
-def make_pool(mode, clients, reqs):
+def make_pool(mode, clients, reqs, handover="early"):
     if mode in ("gpu_batched", "gpu_batched_overlap"):
         pool = Pool(factory(clients, CoreAuthNr), n=4, batched=True, digest_fn=digest.request_digests,
-                    overlap=mode == "gpu_batched_overlap")
+                    overlap=mode == "gpu_batched_overlap", handover=handover)
     elif mode == "no_verify_ceiling":
         # verification AND request digests free: digests looked up in a table
         # made before the run, so this is the harness's own ceiling
@@ -91,9 +91,10 @@ def make_pool(mode, clients, reqs):
     return pool
 
 
-def run(mode, clients, reqs, rate=None):
-    """One pool run: the whole flood at once, or offered at `rate` requests/s."""
-    pool = make_pool(mode, clients, reqs)
+def run(mode, clients, reqs, rate=None, handover="early"):
+    """One pool run: the whole flood at once, or offered at `rate` requests/s;
+    handover: the overlap mode's (Pool docstring)."""
+    pool = make_pool(mode, clients, reqs, handover)
     native = base58._native
     if mode == "cpu_reference":  # the reference's pure-Python base58 / serializer
         base58._native = signing_serializer._native = None

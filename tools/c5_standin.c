@@ -31,3 +31,4 @@ int standin_submit(const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs,
 }
 
 int standin_wait(int device, int64_t ticket) { (void)device; (void)ticket; return 0; }
+int standin_query(int device, int64_t ticket) { (void)device; (void)ticket; return 0; }

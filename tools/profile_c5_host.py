@@ -44,6 +44,7 @@ def standin():
 
 SI = standin()
 ADDRS = tuple(ctypes.cast(getattr(SI, f), ctypes.c_void_p).value for f in ("standin_submit", "standin_wait"))
+QUERY = ctypes.cast(SI.standin_query, ctypes.c_void_p).value
 
 
 def flood(n, seed=0xC5):
@@ -131,6 +132,7 @@ def main():
     edv.BATCH_DEVICE = 0
     edv.verify_address = lambda: ADDRS[0]
     edv.native_batch_enabled = lambda: True
+    edv.query_address = lambda: QUERY
     if "--submit" in sys.argv:
         for b in (100, 400, 1000, 4000):
             print(json.dumps(submit_bench(b)))
