@@ -34,18 +34,21 @@ class GenClock:
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
-    modes = sys.argv[2:] or ["gpu_batched_overlap", "no_verify_ceiling"]
+    # MODE: bench_pool mode, or gpu_batched_overlap:next / :early (the hand-over)
+    modes = sys.argv[2:] or ["gpu_batched_overlap:early", "gpu_batched_overlap:next", "no_verify_ceiling"]
     clients, reqs = bench_pool.make_flood(n)
-    for mode in modes:
-        bench_pool.run(mode, clients, reqs[:500])
+    for spec in modes:
+        mode, _, ho = spec.partition(":")
+        ho = ho or "early"
+        bench_pool.run(mode, clients, reqs[:500], handover=ho)
         gc.collect()
         clk = GenClock()
         gc.callbacks.append(clk)
         try:
-            st = bench_pool.run(mode, clients, reqs)
+            st = bench_pool.run(mode, clients, reqs, handover=ho)
         finally:
             gc.callbacks.remove(clk)
-        print(json.dumps({"mode": mode, "ordered_req_per_s": round(st["ordered_req_per_s_one_process"]),
+        print(json.dumps({"mode": spec, "ordered_req_per_s": round(st["ordered_req_per_s_one_process"]),
                           "wall_s": round(st["wall_s"], 4), "gc_share": round(st["gc_share_of_node_time"], 4),
                           "auth_share": round(st["auth_share_of_node_time"], 4),
                           "collections": clk.n, "gc_s": [round(x, 4) for x in clk.s], "collected": clk.collected,
