@@ -23,7 +23,8 @@
  *
  * All entry points return 0 on success or a negative EDV_E_* code, never
  * throw, and keep no pointer to caller memory after returning (except
- * edv_verify_batch_async, until edv_wait_async for that batch returns).
+ * edv_verify_batch_async, until edv_wait_async -- or edv_query_async returning
+ * anything but EDV_PENDING -- for that batch).
  */
 #ifndef EDV_H
 #define EDV_H
@@ -83,7 +84,7 @@ int edv_verify_batch(const uint8_t *sigs, const uint8_t *pks, const uint8_t *msg
  * this call) run while batch k computes: back to back, the host path then runs
  * at the kernels' rate rather than copy + kernels.  The caller's buffers must
  * stay valid and unchanged, and `accept` unread, until edv_wait_async(device,
- * ticket) returns 0; a submission waits for the batch eight submissions back
+ * ticket) (or edv_query_async) returns 0; a submission waits for the batch eight submissions back
  * (completing it as edv_wait_async would) before reusing its slot.  Same
  * verdicts, arguments and alignment rules as edv_verify_batch.
  */
