@@ -20,6 +20,14 @@ request signatures are verified, and reduces the rest to message counting:
 Not modelled (out of scope): view change, checkpoints,
 catch-up, BLS multi-signatures, ledgers/state execution, client replies.
 
+Fault injection as in the reference's signing test (plenum/test/signing/
+test_signing.py:30-77 with malicious_behaviors_node.py:31-44 changesRequest):
+a node named in Pool(..., alters_propagates={...}) puts a random "amount" into
+the operation of every request it PROPAGATEs, so the client's signature no
+longer matches; the other nodes' authentication of those PROPAGATEs fails with
+InsufficientCorrectSignatures(0, 1), they record the sender as suspicious
+(Node.reportSuspiciousNode) and do not count its vote.
+
 Request latency (what the reference's Monitor acts on, plenum/server/monitor.py:
 300-330 requestOrdered, :418-460 LAMBDA / OMEGA checks) is recorded per request
 and node: from forwarding (f+1 PROPAGATE votes, propagator.py:236-249, where
@@ -47,6 +55,7 @@ order.
 import gc
 import hashlib
 import json
+import random
 import time
 from collections import deque
 
@@ -138,8 +147,12 @@ class _TimedAuth:
 class PoolNode:
     def __init__(self, name, peers, authenticator, f, batched=True, digest_fn=cpu_digests,
                  client_quota=DEFAULT_LISTENER_QUOTA, node_quota=DEFAULT_LISTENER_QUOTA, max_batch=1000,
-                 overlap=False, handover="early"):
+                 overlap=False, handover="early", alters_propagates=False):
         self.name, self.peers, self.f = name, list(peers), f
+        # fault injection: this node's PROPAGATEs carry an altered request
+        # (malicious_behaviors_node.py:31-44 changesRequest)
+        self.alters_propagates = alters_propagates
+        self._rng = random.Random(name)
         self.overlap = overlap and batched
         if handover not in ("early", "next"):
             raise ValueError("handover must be 'early' or 'next'")
@@ -173,6 +186,7 @@ class PoolNode:
         self.ordered = 0
         self.nacks = 0
         self.bad_propagates = 0
+        self.suspicions = []          # (sender, reason) per PROPAGATE that failed authentication
         self.verifies = 0
         self.auth_calls = 0
         self.busy_s = 0.0
@@ -261,8 +275,10 @@ class PoolNode:
 
     def _on_propagate(self, msg, frm, outcome):
         key = next(self._keys)
-        if failed(outcome):
+        ex = failed(outcome)
+        if ex is not None:
             self.bad_propagates += 1  # SuspiciousNode
+            self.suspicions.append((frm, getattr(ex, "reason", str(ex))))   # Node.reportSuspiciousNode
             return
         if key in self.ordered_keys:
             return
@@ -285,6 +301,8 @@ class PoolNode:
         if not st.propagated:
             st.propagated = True
             st.votes.add(self.name)
+            if self.alters_propagates:  # changesRequest: the signature no longer matches
+                req = dict(req, operation=dict(req.get("operation") or {}, amount=self._rng.randint(10, 100000)))
             self.send_all({"op": "PROPAGATE", "request": req, "senderClient": client})
         if not st.forwarded and len(st.votes) >= self.f + 1:   # Quorums.propagate = f + 1
             st.forwarded = True
@@ -372,11 +390,13 @@ class Pool:
     """n nodes (f = (n - 1) // 3), primary = the first; `auth_factory(name)`
     returns each node's ReqAuthenticator."""
 
-    def __init__(self, auth_factory, n=4, batched=True, digest_fn=cpu_digests, overlap=False, **node_kw):
+    def __init__(self, auth_factory, n=4, batched=True, digest_fn=cpu_digests, overlap=False, alters_propagates=(),
+                 **node_kw):
         names = NAMES[:n]
         f = (n - 1) // 3
         self.nodes = {nm: PoolNode(nm, [p for p in names if p != nm], auth_factory(nm), f, batched, digest_fn,
-                                   overlap=overlap, **node_kw) for nm in names}
+                                   overlap=overlap, alters_propagates=nm in alters_propagates, **node_kw)
+                      for nm in names}
         self.nodes[names[0]].is_primary = True
         self.gc_clock = _GcClock()
         for nd in self.nodes.values():

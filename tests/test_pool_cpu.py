@@ -176,3 +176,50 @@ def test_pool_paced_run_records_request_latency(batched, overlap, monkeypatch):
         assert 0 <= lat[kind]["p50"] <= lat[kind]["p99"] <= lat[kind]["max"]
     assert lat["receipt"]["mean"] >= lat["monitor"]["mean"]
     assert lat["submit"]["mean"] >= lat["receipt"]["mean"]
+
+
+@pytest.mark.parametrize("mode", ["sequential", "batched", "overlap_native"])
+def test_pool_node_altering_propagates_is_suspected(mode, monkeypatch):
+    """The reference's signing test (plenum/test/signing/test_signing.py:30-77:
+    evil Alpha with changesRequest, malicious_behaviors_node.py:31-44): every
+    PROPAGATE Alpha sends carries its request with a random "amount" in the
+    operation.  Each good node authenticates those as
+    InsufficientCorrectSignatures(0, 1), suspects Alpha with exactly that reason
+    and does not count its vote; every valid request is still ordered on every
+    node (the honest nodes' f + 1 PROPAGATEs), and Alpha suspects no one -- one
+    message at a time, batched per prod, and overlapped through the native
+    asynchronous path (early hand-over)."""
+    from indy_plenum_amd.exceptions import InsufficientCorrectSignatures
+    monkeypatch.setattr(edv, "open_batch", lambda items, device_mask=0: H.oracle_open_batch(list(items)))
+    if mode == "overlap_native":
+        from test_host_native import _oracle_async_callbacks, _query_address
+        cbs, addrs, _issued = _oracle_async_callbacks([])
+        monkeypatch.setattr(edv, "async_addresses", lambda: addrs)
+        monkeypatch.setattr(edv, "query_address", _query_address(cbs))
+        monkeypatch.setattr(edv, "BATCH_DEVICE", 0)
+        monkeypatch.setattr(edv, "verify_address", lambda: addrs[0])
+        monkeypatch.setattr(edv, "_OPEN_BATCH", H.oracle_open_batch)
+    signers, reqs, valid = flood(n_valid=40, n_bad_sig=6, n_unknown=2, seed=21)
+    pool = Pool(factory(signers), n=4, batched=mode != "sequential", digest_fn=cpu_digests,
+                overlap=mode == "overlap_native", client_quota=16, max_batch=7, alters_propagates={"Alpha"})
+    pool.submit(reqs)
+    try:
+        wall = pool.run(len(valid))
+        for _ in range(20):                                 # let the last PROPAGATEs in flight arrive
+            for nd in pool.nodes.values():
+                nd.prod(pool)
+        pool.drain()
+    finally:
+        pool.close()
+    st = pool.stats(wall, len(valid))
+    assert st["ordered_per_node"] == [len(valid)] * 4
+    assert st["nacks_per_node"] == [len(reqs) - len(valid)] * 4
+    keys = [nd.ordered_keys for nd in pool.nodes.values()]
+    assert all(k == keys[0] for k in keys) and keys[0] == set(cpu_digests(valid))
+    reason = InsufficientCorrectSignatures.reason.format(0, 1)
+    for nd in pool.nodes.values():
+        if nd.name == "Alpha":
+            assert nd.suspicions == []
+        else:   # one altered PROPAGATE per valid request, all from Alpha, all for that reason
+            assert nd.suspicions == [("Alpha", reason)] * len(valid), nd.name
+    assert st["bad_propagates"] == 3 * len(valid)

@@ -95,3 +95,46 @@ def test_pool_c5_gpu_large_flood_equals_reference_flow(monkeypatch, overlap):
     assert gpu["bad_propagates"] == ref["bad_propagates"] == 0
     assert gpu["ordered_keys"] == ref["ordered_keys"]
     assert gpu["verifies"] == ref["verifies"] == 4 * len(reqs) + 4 * 3 * len(valid)
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_pool_gpu_node_altering_propagates_is_suspected(monkeypatch, overlap):
+    """The reference's signing test on the GPU path (plenum/test/signing/
+    test_signing.py:30-77, changesRequest): Alpha alters the request in every
+    PROPAGATE it sends; the GPU-authenticated good nodes raise
+    InsufficientCorrectSignatures(0, 1) for each, suspect Alpha for that reason
+    and still order every valid request -- the same ordered set, NACKs and
+    suspicions as the reference flow (one verifySignature per message on the
+    oracle)."""
+    from indy_plenum_amd.exceptions import InsufficientCorrectSignatures
+    signers, reqs, valid = flood(n_valid=300, n_bad_sig=30, n_unknown=10, seed=77)
+
+    def run(batched, digest_fn, overlap=False):
+        pool = Pool(factory(signers), n=4, batched=batched, digest_fn=digest_fn, overlap=overlap, client_quota=50,
+                    max_batch=40, alters_propagates={"Alpha"})
+        pool.submit(reqs)
+        try:
+            wall = pool.run(len(valid))
+            for _ in range(20):
+                for nd in pool.nodes.values():
+                    nd.prod(pool)
+            pool.drain()
+        finally:
+            pool.close()
+        st = pool.stats(wall, len(valid))
+        st["ordered_keys"] = [sorted(nd.ordered_keys) for nd in pool.nodes.values()]
+        st["suspicions"] = {nd.name: sorted(nd.suspicions) for nd in pool.nodes.values()}
+        return st
+    with monkeypatch.context() as m:
+        m.setattr(edv, "open_batch", H.oracle_open_batch)
+        ref = run(False, cpu_digests)
+    gpu = run(True, digest.request_digests, overlap)
+    assert gpu["ordered_per_node"] == ref["ordered_per_node"] == [len(valid)] * 4
+    assert gpu["nacks_per_node"] == ref["nacks_per_node"]
+    assert gpu["ordered_keys"] == ref["ordered_keys"]
+    assert set(gpu["ordered_keys"][0]) == set(cpu_digests(valid))
+    reason = InsufficientCorrectSignatures.reason.format(0, 1)
+    assert gpu["suspicions"] == ref["suspicions"]
+    assert gpu["suspicions"]["Alpha"] == []
+    for name in ("Beta", "Gamma", "Delta"):
+        assert gpu["suspicions"][name] == [("Alpha", reason)] * len(valid)
