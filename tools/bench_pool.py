@@ -173,7 +173,9 @@ def c5(n=20000, n_cpu=2000, rounds=C5_ROUNDS):
     for m in modes:
         rs = sorted(runs[m], key=lambda st: st["ordered_req_per_s_one_process"])
         out[m] = dict(rs[len(rs) // 2], median_of=len(rs),
-                      runs_ordered_req_per_s=[st["ordered_req_per_s_one_process"] for st in runs[m]])
+                      runs_ordered_req_per_s=[st["ordered_req_per_s_one_process"] for st in runs[m]],
+                      runs=[{k: st[k] for k in ("wall_s", "auth_share_of_node_time", "gc_share_of_node_time",
+                                                "max_node_busy_s", "early_handovers")} for st in runs[m]])
     out["overlap_vs_ceiling_per_round"] = [o["ordered_req_per_s_one_process"] / c["ordered_req_per_s_one_process"]
                                            for o, c in zip(runs["gpu_batched_overlap"], runs["no_verify_ceiling"])]
     if os.path.exists(NOVERIFY_LIB):
