@@ -49,7 +49,7 @@ extern "C" {
  * starts as each slice lands), then the main kernel, which writes the
  * verdicts straight into page-locked host memory (no D2H copy).  A larger
  * shard alternates two streams of half-chunk sub-batches, so the copies of
- * one overlap the kernels of the other.  A shard of at most 8,192 requests
+ * one overlap the kernels of the other.  A shard of at most 16,384 requests
  * (a Node's prod, one Verifier.verify) takes the latency path instead
  * (edv_set_latency_path): one kernel launch with sixteen lanes per signature
  * (eight above 4,096 requests);
@@ -194,7 +194,7 @@ int edv_set_chunk(int device, uint64_t chunk);
 int edv_set_host_slices(int device, int slices);
 
 /* The latency path: every batch of at most max_requests requests (default and
- * at most 8,192; 0 = never) on `device` -- synchronous, asynchronous and
+ * at most 16,384; 0 = never) on `device` -- synchronous, asynchronous and
  * device-resident calls alike -- runs as ONE kernel launch with several lanes
  * per signature (edv_quad.hip; each point doubling and addition split over a
  * quad of lanes, operands exchanged by DPP): up to 4,096 requests sixteen lanes

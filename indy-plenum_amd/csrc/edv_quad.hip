@@ -1,7 +1,7 @@
 // edv_quad.hip -- the latency path: one kernel launch verifies a small batch
 // (a Node's prod, a single Verifier.verify) with several lanes per signature:
 // edv_rtl_kernel (sixteen lanes, no tables, at most 4,096 requests: below) and
-// edv_quad_kernel (eight lanes, per-signature tables, up to 8,192 requests),
+// edv_quad_kernel (eight lanes, per-signature tables, up to 16,384 requests),
 // described first.
 //
 // The batch path (edv_prep.hip, edv_verify.hip) runs one signature per lane:

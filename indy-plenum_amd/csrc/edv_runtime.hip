@@ -98,13 +98,17 @@ constexpr int kAsyncSlots = 8;
 // small is one wave per SIMD on a few SIMDs, and its latency (one main-kernel
 // walk, ~0.45 ms) is all it costs.  Larger batches share the chunk scratch.
 constexpr uint64_t kSmallAsync = 8192;
-// The latency path (edv_quad.hip: one launch, four lanes per signature) takes
-// every batch of at most this many requests on the host paths and the
-// device-resident path (edv_set_latency_path changes it per device; 0 = off).
-// Below one wave per SIMD the batch kernels' time is one lane's serial chain
-// whatever n is; the quad kernel splits each point operation over four lanes.
-constexpr uint64_t kQuadMaxDefault = 8192;  // profiles/r06/latency_paths_s3.jsonl: faster than the batch kernels at every n up to 8,192
-constexpr uint64_t kQuadMaxLimit = kSmallAsync;  // the async slots' scratch is sized for it
+// The latency path (edv_quad.hip: one launch, sixteen lanes per signature up to
+// 4,096 requests, eight above) takes every batch of at most this many requests
+// on the host paths and the device-resident path (edv_set_latency_path changes
+// it per device; 0 = off).  Below one wave per SIMD the batch kernels' time is
+// one lane's serial chain whatever n is; the latency kernels split each point
+// operation over a quad of lanes.
+// profiles/r06/latency_paths_s3.jsonl: faster than the batch kernels at every n up to 8,192;
+// profiles/r06/quad_limit_s51.jsonl: the two-walk kernel at 12,288 / 16,384 requests 386 / 392 us
+// against 569 / 567 for the batch kernels (two waves per SIMD), level at 20,480, behind at 32,768
+constexpr uint64_t kQuadMaxDefault = 16384;
+constexpr uint64_t kQuadMaxLimit = 16384;  // the quad kernel's per-signature table scratch grows with n (57 MB here)
 
 // One set of per-chunk state buffers (ChunkState storage + bucket permutation)
 // for `cap` signatures (~5.5 kB each: ~1.4 GB for a whole 2^18 chunk).  Sized
@@ -1879,7 +1883,7 @@ int edv_set_latency_path(int device, uint64_t max_requests) {
   int err = 0;
   DevCtx* c = get_ctx(device, &err);
   if (!c) return err;
-  if (max_requests > kQuadMaxLimit) return set_err(EDV_E_ARG, "latency path is for batches of at most 8,192");
+  if (max_requests > kQuadMaxLimit) return set_err(EDV_E_ARG, "latency path is for batches of at most 16,384");
   std::lock_guard<std::mutex> lk(c->mu);
   c->quad_max = max_requests;
   return 0;

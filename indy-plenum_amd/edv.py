@@ -237,7 +237,7 @@ def set_length_buckets(device: int, mode: int):
     _check(lib().edv_set_length_buckets(device, mode))
 
 
-LATENCY_PATH_DEFAULT = 8192
+LATENCY_PATH_DEFAULT = 16384
 
 
 def set_latency_path(device: int, max_requests: int):

@@ -127,7 +127,7 @@ def test_long_and_skewed_message_lengths():
     sigs, pks, msgs, off = _signed_lengths(lens, 0x5A)
     want = checker(sigs, pks, msgs, off)
     assert 0.65 < want.mean() < 0.95
-    assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off), want)   # the latency path (n <= 8,192)
+    assert np.array_equal(edv.verify_arrays(sigs, pks, msgs, off), want)   # the latency path (n <= its default limit)
     try:
         edv.set_latency_path(0, 0)   # the batch kernels, across chunk seams
         for chunk in (256, 1024, 0):
@@ -406,7 +406,7 @@ def test_length_bucket_modes_same_verdicts(mode):
         edv.set_latency_path(0, edv.LATENCY_PATH_DEFAULT)
 
 
-# ---- the latency path (edv_quad.hip): four lanes per signature, one launch
+# ---- the latency path (edv_quad.hip): sixteen / eight lanes per signature, one launch
 @pytest.fixture
 def latency_limit():
     """Set the latency path's batch limit of device 0 for one test, restored after."""
@@ -416,12 +416,12 @@ def latency_limit():
     edv.set_latency_path(0, edv.LATENCY_PATH_DEFAULT)
 
 
-@pytest.mark.parametrize("limit", [0, 8192])
+@pytest.mark.parametrize("limit", [0, 16384])
 def test_golden_on_both_paths(golden, golden_meta, latency_limit, limit):
     """The 3,284 libsodium golden cases (every strictness category: S + kL,
     torsion and mixed-order A accepted iff 8 | h, small-order and non-canonical
     R / A, off-curve points, ...) on the batch kernels (limit 0) and on the
-    latency kernel (limit 8,192: the whole set in one launch), and the
+    latency kernel (limit 16,384: the whole set in one launch), and the
     positional-split cases through open_batch."""
     latency_limit(limit)
     sigs, pks, msgs, off = golden_io.pack_batch(golden)
@@ -438,16 +438,20 @@ def test_latency_path_batch_sizes_and_entry_points(latency_limit):
     16-slot padding of tiny batches and its limit, variable message lengths (200..4,096 B) and 20 % damage, through the
     synchronous call, the asynchronous one (pageable and page-locked verdicts)
     and the device-resident one with a non-zero msg_base; verdicts equal
-    libsodium's (the oracle where it is absent)."""
-    latency_limit(8192)
-    sigs, pks, msgs, off = orc.corpus(0x1A7, 0, 8192, mode=1, invalid_permille=200)
+    libsodium's (the oracle where it is absent).  Up to the default limit,
+    16,384 requests (the two-walk kernel above 4,096 at two waves per SIMD)."""
+    latency_limit(edv.LATENCY_PATH_DEFAULT)
+    N = edv.LATENCY_PATH_DEFAULT
+    sigs, pks, msgs, off = orc.corpus(0x1A7, 0, N, mode=1, invalid_permille=200)
     want = checker(sigs, pks, msgs, off)
-    for n in (1, 2, 3, 4, 5, 15, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 129, 400, 1000, 4095, 4096, 4097, 8192):
+    for n in (1, 2, 3, 4, 5, 15, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 129, 400, 1000, 4095, 4096, 4097, 8192,
+              8193, 12289, N - 1, N):
         o = off[:n + 1]
         got = edv.verify_arrays(sigs[:64 * n], pks[:32 * n], msgs, o)
         assert np.array_equal(got, want[:n]), n
-    pin = edv.PinnedBuffer(8192)
-    for n, acc in ((400, np.zeros(400, np.uint8)), (8192, pin.array[:8192])):
+    pin = edv.PinnedBuffer(N)
+    for n, acc in ((400, np.zeros(400, np.uint8)), (8192, pin.array[:8192]), (N, np.zeros(N, np.uint8)),
+                   (N, pin.array[:N])):
         ts = [edv.verify_async(sigs[:64 * n], pks[:32 * n], msgs, off[:n + 1], acc) for _ in range(1)]
         for t in ts:
             edv.wait_async(t)
@@ -469,8 +473,8 @@ def test_latency_path_on_corpus_bitmask_slices(latency_limit):
     """The latency kernel against libsodium's committed corpus bitmasks: the
     first 2^18 requests of the C2 corpus (256 B) and of the C4 corpus
     (200..4,096 B, 5 % invalid over every damage kind), in 4,096-request calls
-    (the default limit), slice hashes checked first."""
-    latency_limit(4096)
+    (the right-to-left kernel) and in 16,384-request calls (the two-walk
+    kernel at the default limit), slice hashes checked first."""
     meta = _bitmask_meta()
     for name in ("c2_256B", "c4_var"):
         cfg = meta["corpora"][name]
@@ -478,9 +482,11 @@ def test_latency_path_on_corpus_bitmask_slices(latency_limit):
         sigs, pks, msgs, off = orc.corpus(cfg["seed"], 0, n, cfg["mode"], cfg["invalid_permille"])
         bits = np.fromfile(os.path.join(GOLDEN, "corpus_%s.bits" % name), dtype=np.uint8)
         want = np.unpackbits(bits[:n // 8], bitorder="little")
-        got = np.zeros(n, np.uint8)
-        for lo in range(0, n, 4096):
-            got[lo:lo + 4096] = edv.verify_arrays(sigs[64 * lo:64 * (lo + 4096)], pks[32 * lo:32 * (lo + 4096)],
-                                                  msgs, off[lo:lo + 4097])
-        mism = np.nonzero(got != want)[0]
-        assert mism.size == 0, (name, mism[:10].tolist())
+        for step in (4096, 16384):   # the right-to-left kernel, then the two-walk kernel at two waves per SIMD
+            latency_limit(step)
+            got = np.zeros(n, np.uint8)
+            for lo in range(0, n, step):
+                got[lo:lo + step] = edv.verify_arrays(sigs[64 * lo:64 * (lo + step)], pks[32 * lo:32 * (lo + step)],
+                                                      msgs, off[lo:lo + step + 1])
+            mism = np.nonzero(got != want)[0]
+            assert mism.size == 0, (name, step, mism[:10].tolist())

@@ -36,7 +36,7 @@ def gpu_present():
 def batch_kernels_for_small_batches():
     """This module tests the batch kernels' host-path mechanics (field slices,
     sub-batches, chunk seams, slot streams) on batches that the latency path
-    (edv_set_latency_path, default: up to 8,192 requests) would otherwise take:
+    (edv_set_latency_path, default: up to 16,384 requests) would otherwise take:
     here it is off on device 0; test_gpu_parity.py and the fault-hook test
     below cover the latency path."""
     edv.set_latency_path(0, 0)
