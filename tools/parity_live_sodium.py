@@ -14,7 +14,7 @@ tests/test_gpu_parity.py with fresh corpora of a different generator:
       edv_verify_batch, FUZZ_SLICE requests per call, default 2^18 = one chunk:
       the field-ordered path with staged message quarters)
 
-  latency  requests sent in calls of 1..8,192 requests (random sizes), i.e.
+  latency  requests sent in calls of 1..LATENCY_PATH_DEFAULT requests (random sizes), i.e.
       through the latency kernel (csrc/edv_quad.hip): half fuzzed 256-B
       requests as above, half C4-style 200..4,096-B requests, 5 % damaged
       over seven kinds
@@ -121,8 +121,8 @@ def fuzz(total, seed=0xF022):
 def latency(total, seed=0x1A7E):
     """The latency kernel: slices of 2^18 requests (alternately fuzzed 256-B
     and C4-style 200..4,096-B with seven damage kinds) sent through
-    edv_verify_batch in calls of random size 1..8,192 (every call at or below
-    the default latency-path limit), all verdicts against libsodium live."""
+    edv_verify_batch in calls of random size 1..edv.LATENCY_PATH_DEFAULT
+    (16,384: every call on the latency path), all verdicts against libsodium live."""
     from indy_plenum_amd import edv
     t0 = time.time()
     rng = np.random.default_rng(seed)
@@ -141,7 +141,7 @@ def latency(total, seed=0x1A7E):
         got = np.zeros(n, np.uint8)
         lo = 0
         while lo < n:
-            m = min(n - lo, int(rng.integers(1, 8193)))
+            m = min(n - lo, int(rng.integers(1, edv.LATENCY_PATH_DEFAULT + 1)))
             o = off[lo:lo + m + 1]
             got[lo:lo + m] = edv.verify_arrays(sigs[64 * lo:64 * (lo + m)], pks[32 * lo:32 * (lo + m)], msgs, o)
             lo += m
@@ -153,7 +153,8 @@ def latency(total, seed=0x1A7E):
         mism += int(bad.size)
         checked += n
         rejected += int(n - want.sum())
-    out = {"workload": "latency path: fuzzed 256-B and C4-style 200..4,096-B requests in calls of 1..8,192",
+    out = {"workload": "latency path: fuzzed 256-B and C4-style 200..4,096-B requests in calls of 1..%d"
+                       % edv.LATENCY_PATH_DEFAULT,
            "requests": checked, "calls": calls, "libsodium_rejected": rejected, "mismatches": mism,
            "first_mismatch": first_bad, "seconds": round(time.time() - t0, 1)}
     print(json.dumps(out), flush=True)
