@@ -153,7 +153,7 @@ def run_isolated(mode, n, lib):
     return st
 
 
-C5_ROUNDS = 3
+C5_ROUNDS = 5
 
 
 def c5(n=20000, n_cpu=2000, rounds=C5_ROUNDS):
