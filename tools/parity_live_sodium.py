@@ -20,6 +20,8 @@ tests/test_gpu_parity.py with fresh corpora of a different generator:
       over seven kinds
 
   python tools/parity_live_sodium.py [c3_total] [c4_total] [fuzz_total] [latency_total]
+LIVE_SEED=k (default 0) XORs k into every corpus seed: a rerun with a new k checks
+fresh keys, messages and damage instead of repeating the corpora already recorded.
 Prints one JSON line per workload and a summary; exit status 1 on any mismatch.
 """
 import json
@@ -36,6 +38,8 @@ import oracle_lib as orc  # noqa: E402  (libsodium harness: the checker)
 from indy_plenum_amd import workload  # noqa: E402
 
 SLICE = 1 << 20
+SEED = int(os.environ.get("LIVE_SEED", "0"), 0)
+BENCH_SEED = 0x5EED2025  # workload.DeviceBatch's default
 
 
 def run(name, total, **kw):
@@ -91,7 +95,7 @@ def fuzzed(n, start, seed, rng):
     return sigs.reshape(-1), pks.reshape(-1), msgs, off
 
 
-def fuzz(total, seed=0xF022):
+def fuzz(total, seed=0xF022 ^ SEED):
     """Random damage anywhere (fuzzed()), verified through the C-ABI host path
     (edv_verify_batch on host buffers)."""
     from indy_plenum_amd import edv
@@ -118,7 +122,7 @@ def fuzz(total, seed=0xF022):
     return out
 
 
-def latency(total, seed=0x1A7E):
+def latency(total, seed=0x1A7E ^ SEED):
     """The latency kernel: slices of 2^18 requests (alternately fuzzed 256-B
     and C4-style 200..4,096-B with seven damage kinds) sent through
     edv_verify_batch in calls of random size 1..edv.LATENCY_PATH_DEFAULT
@@ -134,7 +138,7 @@ def latency(total, seed=0x1A7E):
         if k % 2 == 0:
             sigs, pks, msgs, off = fuzzed(n, start, seed, rng)
         else:
-            b = workload.DeviceBatch(n, start=start, seed=0xC4C4, keep_host=True, var_range=(200, 4096),
+            b = workload.DeviceBatch(n, start=start, seed=0xC4C4 ^ SEED, keep_host=True, var_range=(200, 4096),
                                      damage_every=20, damage_kinds=7)
             sigs, pks, msgs, off = b.host_copy()
             del b
@@ -168,13 +172,13 @@ def main():
     c4 = int(sys.argv[2]) if len(sys.argv) > 2 else 4194304
     nf = int(sys.argv[3]) if len(sys.argv) > 3 else 2097152
     nl = int(sys.argv[4]) if len(sys.argv) > 4 else 1048576
-    res = [run("C3 256 B, 5 % damaged (4 kinds)", c3, damage_every=20, damage_kinds=4),
-           run("C4 200..4,096 B, 5 % damaged (7 kinds)", c4, seed=0xC4C4, var_range=(200, 4096), damage_every=20,
+    res = [run("C3 256 B, 5 % damaged (4 kinds)", c3, seed=BENCH_SEED ^ SEED, damage_every=20, damage_kinds=4),
+           run("C4 200..4,096 B, 5 % damaged (7 kinds)", c4, seed=0xC4C4 ^ SEED, var_range=(200, 4096), damage_every=20,
                damage_kinds=7),
            fuzz(nf), latency(nl)]
     total = sum(r["requests"] for r in res)
     bad = sum(r["mismatches"] for r in res)
-    print(json.dumps({"summary": "GPU vs libsodium 1.0.18, live", "requests": total, "mismatches": bad}))
+    print(json.dumps({"summary": "GPU vs libsodium 1.0.18, live", "live_seed": SEED, "requests": total, "mismatches": bad}))
     sys.exit(1 if bad else 0)
 
 
